@@ -1,0 +1,44 @@
+"""Shared pytest setup: paths, the `gpu` marker, golden-fixture loading."""
+from __future__ import annotations
+
+import glob
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG_DIR = os.path.join(ROOT, "minesweeper-ppo_amd")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+for p in (ROOT, PKG_DIR, os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+
+
+def golden(name: str):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+def golden_files(pattern: str):
+    return sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, pattern)))
+
+
+def has_gpu() -> bool:
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    if not has_gpu():
+        pytest.fail("gpu-marked test ran without a HIP device (run with -m 'not gpu' on CPU)")
+    import torch
+    return torch.device("cuda:0")

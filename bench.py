@@ -1,0 +1,190 @@
+"""Benchmark: env steps/sec of the HIP board step on BASELINE.json's config
+(16x16x40, N=4096 envs per GPU; weak scaling over ranks), with the dominant
+kernel's HBM roofline fraction and the CPU restatement timed on this host.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+A step = one synthetic-policy action pass (ms_tape_actions) + one board step
+(ms_step, all outputs: obs, mask, reward, done, aux) over every env of the
+rank. Inputs are resident in HBM; the timed region is bracketed by a barrier
+and torch.cuda.synchronize() on both sides; the MAX over ranks is reported.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "minesweeper-ppo_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
+
+
+def algo_bytes_per_env_step(H: int, W: int) -> int:
+    """obs 40HW + mask HW + action 8 + reward 4 + done 1 + aux 12
+    + packed board state read+write 2*(2*ceil(HW/8) + 32) + PCG inc read 16."""
+    A = H * W
+    return 40 * A + A + 8 + 4 + 1 + 12 + 2 * (2 * ((A + 7) // 8) + 32) + 16
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--board", default="16x16x40")
+    ap.add_argument("--tape", type=int, default=0, help="0 uniform-valid, 1 safe-biased")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
+    return ap.parse_args()
+
+
+def cpu_baseline(H, W, K, n_envs, seed, tape, budget_s, threads):
+    """Oracle (CPU restatement, C + pthreads) timed on this host, bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    O.build()
+    v = O.OracleVec(H, W, K, n_envs, seed=seed)
+    v.reset()
+    A = H * W
+    obs = np.zeros((n_envs, 10, H, W), np.float32)
+    mask = np.zeros((n_envs, A), np.uint8)
+    rew = np.zeros(n_envs, np.float32)
+    done = np.zeros(n_envs, np.uint8)
+    st = np.zeros(n_envs, np.int32)
+    ln = np.zeros(n_envs, np.int32)
+    fr = np.zeros(n_envs, np.float64)
+    oc = np.zeros(n_envs, np.int8)
+    act = np.zeros(n_envs, np.int64)
+    for t in range(5):  # warm-up (page in buffers)
+        v.tape(t, tape, out=act)
+        v.step_into(act, obs, mask, rew, done, st, ln, fr, oc, nthreads=threads)
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        v.tape(5 + steps, tape, out=act)
+        v.step_into(act, obs, mask, rew, done, st, ln, fr, oc, nthreads=threads)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s and steps >= 3:
+            break
+    return dict(value=n_envs * steps / el, unit="env_steps/s", cores=threads, kind="port",
+                sample=f"{steps} steps x {n_envs} envs {H}x{W}x{K} (tape {tape}) in {el:.1f}s, "
+                       f"oracle/ms_oracle.c on {threads} pthreads")
+
+
+def main():
+    args = parse()
+    H, W, K = (int(x) for x in args.board.lower().split("x"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    from ms_amd import EnvConfig, VecMinesweeper
+
+    n_local = args.envs
+    n_total = n_local * world
+    vec = VecMinesweeper(n_total, EnvConfig(H=H, W=W, mine_count=K), seed=args.seed, device=dev,
+                         shard=(rank, world))
+    assert vec.num_envs == n_local
+    A = H * W
+    obs = torch.empty((n_local, 10, H, W), dtype=torch.float32, device=dev)
+    mask = torch.empty((n_local, A), dtype=torch.bool, device=dev)
+    rew = torch.empty(n_local, dtype=torch.float32, device=dev)
+    done = torch.empty(n_local, dtype=torch.bool, device=dev)
+    step_i = torch.empty(n_local, dtype=torch.int32, device=dev)
+    lnew = torch.empty(n_local, dtype=torch.int32, device=dev)
+    frac = torch.empty(n_local, dtype=torch.float64, device=dev)
+    outc = torch.empty(n_local, dtype=torch.int8, device=dev)
+    act = torch.empty(n_local, dtype=torch.int64, device=dev)
+    lib, h = vec._lib, vec._h
+    from ms_amd import _lib as L
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    ptrs = [L.ptr(x) for x in (act, obs, mask, rew, done, step_i, lnew, frac, outc)]
+
+    def one_step(t, ev=None):
+        L.check(lib.ms_tape_actions(h, t, args.tape, ptrs[0], sp))
+        if ev is not None:
+            ev[0].record(stream)
+        L.check(lib.ms_step(h, *ptrs, sp))
+        if ev is not None:
+            ev[1].record(stream)
+
+    vec.reset(out={"obs": obs, "action_mask": mask})
+    for t in range(args.warmup):
+        one_step(t)
+    torch.cuda.synchronize()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        one_step(args.warmup + k, events[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    total_env_steps = n_total * args.steps
+    value = total_env_steps / elapsed
+    bpe = algo_bytes_per_env_step(H, W)
+    achieved = bpe * n_local / (kern_ms * 1e-3) / 1e9
+
+    out = {
+        "metric": "env steps/sec (16x16x40, N envs) + PPO updates/sec at 1/2/4/8 MI355X",
+        "value": value,
+        "unit": "env_steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8/u64 board bits -> f32 obs",
+        "data": "synthetic: numpy-seeded boards, splitmix64 action tape (SURVEY.md §8d)",
+        "config": {"workload": f"board step {H}x{W}x{K}, {n_local} envs per GPU (BASELINE configs[1]"
+                               f"{', configs[3] at 8 GPUs' if world == 8 else ''})",
+                   "board": f"{H}x{W}x{K}", "envs_per_gpu": n_local, "envs_total": n_total,
+                   "tape": args.tape, "parallelism": f"env-shard x{world}, no collective"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "k_step", "kernel_ms": kern_ms, "algo_bytes_per_env_step": bpe},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        out["cpu_baseline"] = cpu_baseline(H, W, K, n_local, args.seed, args.tape, args.cpu_seconds,
+                                           threads)
+        out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

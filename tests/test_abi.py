@@ -1,0 +1,74 @@
+"""CPU-side checks of the drop-in boundary: libmsenv.so loads, exports every
+symbol include/msenv.h declares, and argument validation fails loudly."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "msenv.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ms_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_expected_entry_points():
+    fns = header_functions()
+    for name in ("ms_create", "ms_destroy", "ms_reset", "ms_step", "ms_step_i32", "ms_labels",
+                 "ms_snapshot", "ms_tape_actions", "ms_gae", "ms_sample_masked", "ms_last_error",
+                 "ms_rng_state", "ms_abi_version"):
+        assert name in fns
+
+
+def test_library_exports_every_header_symbol():
+    from ms_amd import _lib as L
+    lib = L.load()
+    for name in header_functions():
+        assert hasattr(lib, name), name
+        assert name in L.SIGNATURES, f"{name} has no ctypes signature"
+
+
+def test_single_hip_runtime_mapped():
+    from ms_amd import _lib as L
+    L.load()
+    assert len(L._hip_runtimes_mapped()) == 1
+
+
+def test_abi_version_and_error_paths():
+    from ms_amd import _lib as L
+    lib = L.load()
+    assert lib.ms_abi_version() == L.ABI_VERSION
+    h = ctypes.c_void_p()
+    bad = L.MsCfg(100, 16, 40, 1, 1.0, -1.0, 1e-4)  # H > 64: rejected before any HIP call
+    assert lib.ms_create(ctypes.byref(bad), 4, 0, 0, 4, ctypes.byref(h)) == 1
+    assert b"unsupported board" in lib.ms_last_error()
+    ok = L.MsCfg(16, 16, 40, 1, 1.0, -1.0, 1e-4)
+    assert lib.ms_create(ctypes.byref(ok), 4, 0, 2, 4, ctypes.byref(h)) == 1  # range past n_total
+    assert lib.ms_step(None, None, None, None, None, None, None, None, None, None, None) == 1
+    assert b"null handle" in lib.ms_last_error()
+    assert lib.ms_destroy(None) == 0
+    with pytest.raises(L.MsEnvError):
+        L.check(lib.ms_gae(None, None, None, None, 0, 0, 0.0, 0.0, None, None, None))
+
+
+def test_envconfig_matches_reference_fields():
+    from ms_amd import EnvConfig
+    c = EnvConfig()
+    assert (c.H, c.W, c.mine_count, c.guarantee_safe_neighborhood) == (8, 8, 10, True)
+    assert (c.win_reward, c.loss_reward, c.step_penalty) == (1.0, -1.0, 1e-4)
+    with pytest.raises(TypeError):
+        EnvConfig(include_frontier_channel=True)  # unknown keys raise, as in env.py:19-30
+
+
+def test_vec_refuses_cpu_device():
+    from ms_amd import EnvConfig, VecMinesweeper
+    from ms_amd._lib import MsEnvError
+    with pytest.raises(MsEnvError):
+        VecMinesweeper(4, EnvConfig(), device="cpu")

@@ -1,0 +1,187 @@
+"""GPU parity of the HIP board step against the golden fixtures (captured from
+the reference) and against the pinned CPU oracle, through the C ABI."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden, golden_files
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _vec(H, W, K, N, seed=0, **kw):
+    from ms_amd import EnvConfig, VecMinesweeper
+    return VecMinesweeper(N, EnvConfig(H=H, W=W, mine_count=K), seed=seed, **kw)
+
+
+def _codes(obs: torch.Tensor) -> np.ndarray:
+    return O.codes_from_obs(obs.cpu().numpy())
+
+
+@pytest.mark.parametrize("name", [n for n in golden_files("traj_*.npz") if "late" not in n])
+def test_trajectory_golden_gpu(gpu, name):
+    z = golden(name)
+    H, W, K, N, T = (int(z[k]) for k in ("H", "W", "K", "N", "T"))
+    v = _vec(H, W, K, N, seed=int(z["seed"]))
+    d = v.reset()
+    assert np.array_equal(_codes(d["obs"]), z["reset_codes"])
+    mode = int(z["mode"])
+    for t in range(T):
+        a = v.tape_actions(t, mode)
+        assert np.array_equal(a.cpu().numpy(), z["actions"][t]), t
+        batch, r, dn, info = v.step(a)
+        assert np.array_equal(r.cpu().numpy(), z["rewards"][t]), t
+        assert np.array_equal(dn.cpu().numpy(), z["dones"][t]), t
+        tens = info.tensors
+        assert np.array_equal(tens["outcome"].cpu().numpy(), z["outcome"][t]), t
+        assert np.array_equal(tens["step"].cpu().numpy(), z["step"][t]), t
+        assert np.array_equal(tens["last_new_reveals"].cpu().numpy(), z["last_new"][t]), t
+        assert np.array_equal(tens["revealed_frac"].cpu().numpy(), z["frac"][t]), t
+        assert np.array_equal(_codes(batch["obs"]), z["codes"][t]), t
+        assert np.array_equal(batch["action_mask"].cpu().numpy(), z["codes"][t] == 0), t
+        mines = v.snapshot_tensors()["mine"].cpu().numpy().reshape(N, -1)
+        assert np.array_equal(np.packbits(mines, axis=1), z["mines"][t]), t
+    assert np.array_equal(v.rng_state(), z["end_states"])
+
+
+def _diff_run(H, W, K, N, T, mode, seed=0, check_every=1, labels=True):
+    v = _vec(H, W, K, N, seed=seed)
+    o = O.OracleVec(H, W, K, N, seed=seed)
+    d = v.reset()
+    oo, om = o.reset()
+    assert np.array_equal(d["obs"].cpu().numpy(), oo)
+    for t in range(T):
+        a = v.tape_actions(t, mode)
+        a_np = a.cpu().numpy()
+        assert np.array_equal(a_np, o.tape(t, mode)), t
+        if labels and t % 7 == 3:
+            lab, val = v.mine_labels()
+            olab, oval = o.labels()
+            assert np.array_equal(lab.cpu().numpy(), olab) and np.array_equal(val.cpu().numpy(), oval)
+        batch, r, dn, info = v.step(a)
+        ref = o.step(a_np)
+        tens = info.tensors
+        assert np.array_equal(r.cpu().numpy(), ref["reward"]), t
+        assert np.array_equal(dn.cpu().numpy(), ref["done"]), t
+        assert np.array_equal(tens["outcome"].cpu().numpy(), ref["outcome"]), t
+        assert np.array_equal(tens["last_new_reveals"].cpu().numpy(), ref["last_new"]), t
+        assert np.array_equal(tens["revealed_frac"].cpu().numpy(), ref["frac"]), t
+        if t % check_every == 0:
+            assert np.array_equal(batch["obs"].cpu().numpy(), ref["obs"]), t
+            assert np.array_equal(batch["action_mask"].cpu().numpy(), ref["mask"]), t
+    snap = v.snapshot_tensors()
+    osnap = o.snapshot()
+    assert np.array_equal(snap["counts"].cpu().numpy().reshape(N, -1), osnap["counts"])
+    assert np.array_equal(snap["mine"].cpu().numpy().reshape(N, -1), osnap["mine"])
+    assert np.array_equal(snap["step_count"].cpu().numpy(), osnap["step_count"])
+    assert np.array_equal(v.rng_state(), o.rng_state())
+
+
+@pytest.mark.parametrize("H,W,K", [(16, 16, 40), (9, 9, 10), (30, 16, 99), (16, 30, 99), (8, 8, 10)])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_diff_vs_oracle_benchmark_shapes(gpu, H, W, K, mode):
+    _diff_run(H, W, K, N=512, T=120, mode=mode, seed=11)
+
+
+@pytest.mark.parametrize("H,W,K", [(5, 7, 8), (1, 1, 0), (2, 3, 5), (13, 31, 60), (64, 62, 700),
+                                   (64, 1, 10), (1, 62, 12), (4, 4, 15), (6, 6, 0)])
+def test_diff_vs_oracle_generic_shapes(gpu, H, W, K):
+    _diff_run(H, W, K, N=64, T=60, mode=1, seed=5)
+
+
+def test_guarantee_off_and_custom_rewards(gpu):
+    from ms_amd import EnvConfig, VecMinesweeper
+    cfg = EnvConfig(H=8, W=8, mine_count=20, guarantee_safe_neighborhood=False, win_reward=2.5,
+                    loss_reward=-0.75, step_penalty=0.01)
+    v = VecMinesweeper(128, cfg, seed=2)
+    o = O.OracleVec(8, 8, 20, 128, seed=2, guarantee=False, win_reward=2.5, loss_reward=-0.75,
+                    step_penalty=0.01)
+    v.reset()
+    o.reset()
+    for t in range(80):
+        a = v.tape_actions(t, 1)
+        _, r, dn, _ = v.step(a)
+        ref = o.step(a.cpu().numpy())
+        assert np.array_equal(r.cpu().numpy(), ref["reward"])
+        assert np.array_equal(dn.cpu().numpy(), ref["done"])
+
+
+def test_int32_and_wrapped_actions(gpu):
+    v1, v2 = _vec(16, 16, 40, 256, seed=3), _vec(16, 16, 40, 256, seed=3)
+    v1.reset()
+    v2.reset()
+    g = torch.Generator().manual_seed(0)
+    for t in range(30):
+        a = torch.randint(-10_000, 10_000, (256,), generator=g)
+        b1, r1, d1, _ = v1.step(a.to(torch.int32).cuda())
+        b2, r2, d2, _ = v2.step(torch.remainder(a, 256).cuda())
+        assert torch.equal(b1["obs"], b2["obs"]) and torch.equal(r1, r2) and torch.equal(d1, d2)
+
+
+def test_bad_action_shape_asserts(gpu):
+    v = _vec(8, 8, 10, 4)
+    v.reset()
+    with pytest.raises(AssertionError):
+        v.step(np.zeros(5, np.int64))
+
+
+def test_sharded_equals_unsharded(gpu):
+    from ms_amd import EnvConfig, VecMinesweeper
+    cfg = EnvConfig(H=16, W=16, mine_count=40)
+    full = VecMinesweeper(1024, cfg, seed=7)
+    parts = [VecMinesweeper(1024, cfg, seed=7, shard=(r, 4)) for r in range(4)]
+    full.reset()
+    for p in parts:
+        p.reset()
+    for t in range(40):
+        a = full.tape_actions(t, 0)
+        pa = [p.tape_actions(t, 0) for p in parts]
+        assert torch.equal(a, torch.cat(pa))
+        bf, rf, _, _ = full.step(a)
+        outs = [p.step(x) for p, x in zip(parts, pa)]
+        assert torch.equal(bf["obs"], torch.cat([o[0]["obs"] for o in outs]))
+        assert torch.equal(rf, torch.cat([o[1] for o in outs]))
+
+
+def test_full_size_properties(gpu):
+    """BASELINE config C2 (16x16x40, N=4096): size-independent invariants."""
+    N, H, W, K = 4096, 16, 16, 40
+    v = _vec(H, W, K, N, seed=0)
+    d = v.reset()
+    assert torch.count_nonzero(d["obs"]) == 0 and bool(d["action_mask"].all())
+    for t in range(200):
+        a = v.tape_actions(t, 1)
+        batch, r, dn, info = v.step(a)
+        obs, mask = batch["obs"], batch["action_mask"]
+        # one-hot: each revealed cell has exactly one count plane; hidden none
+        rev = obs[:, 0] > 0
+        assert torch.equal(obs[:, 1:].sum(1), rev.float())
+        assert torch.equal(mask.view(N, H, W), ~rev)
+        # done envs come back fresh
+        assert torch.count_nonzero(obs[dn]) == 0
+        # rewards take only the three reference values
+        vals = torch.unique(r).cpu().numpy()
+        allowed = {np.float32(-1e-4), np.float32(-1.0 - 1e-4), np.float32(1.0 - 1e-4)}
+        assert set(vals.tolist()) <= {float(x) for x in allowed}
+    snap = v.snapshot_tensors()
+    fc = snap["first_click"]
+    assert torch.equal(snap["mine"][fc].sum((1, 2)), torch.full((int(fc.sum()),), K, device=gpu,
+                                                                dtype=torch.int64))
+    assert not bool(snap["mine"][~fc].any())
+
+
+def test_numpy_compat_mode(gpu):
+    v = _vec(9, 9, 10, 16, as_numpy=True)
+    d = v.reset()
+    assert isinstance(d["obs"], np.ndarray) and d["obs"].dtype == np.float32
+    assert d["action_mask"].dtype == bool and d["action_mask"].shape == (16, 81)
+    b, r, dn, info = v.step(np.zeros(16, np.int32))
+    assert r.dtype == np.float32 and dn.dtype == bool
+    assert len(info["aux"]) == 16 and set(info["aux"][0]) == {"step", "last_new_reveals", "revealed_frac"}
+    assert all(o is None or o in ("win", "loss") for o in info["outcome"])
+    e = v.envs[3]
+    assert e.first_click_done and e.revealed.shape == (9, 9) and e.mine_mask.sum() == 10
+    assert (e.adjacent_counts <= 8).all() and not e.flags.any()

@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
+    ap.add_argument("--diag-no-obs", action="store_true", help="diagnostic: skip obs/mask outputs")
     return ap.parse_args()
 
 
@@ -118,6 +119,8 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
     ptrs = [L.ptr(x) for x in (act, obs, mask, rew, done, step_i, lnew, frac, outc)]
+    if args.diag_no_obs:
+        ptrs[1] = ptrs[2] = None
 
     def one_step(t, ev=None):
         L.check(lib.ms_tape_actions(h, t, args.tape, ptrs[0], sp))

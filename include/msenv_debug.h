@@ -1,0 +1,29 @@
+/*
+ * msenv_debug.h — test/diagnostic hooks of libmsenv.so (not part of the
+ * drop-in boundary; bench.py and the GPU tests use them).
+ */
+#ifndef MSENV_DEBUG_H
+#define MSENV_DEBUG_H
+
+#include <stdint.h>
+
+#include "msenv.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* debug flags */
+#define MS_DBG_FORCE_SERIAL_PLACEMENT 1u /* skip the lane-parallel PCG/Floyd path */
+
+int ms_set_debug_flags(ms_handle* h, uint32_t flags);
+
+/* libmsenv_diag.so only: per-env s_memtime/s_memrealtime stamps, device
+ * u64[env_count][8] (NULL disables). Ignored by the production build. */
+int ms_set_diag(ms_handle* h, uint64_t* stamps);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MSENV_DEBUG_H */

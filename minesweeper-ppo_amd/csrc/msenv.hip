@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "../../include/msenv.h"
+#include "../../include/msenv_debug.h"
 
 namespace {
 
@@ -67,6 +68,9 @@ struct KParams {
   int32_t H, W, K, guarantee;
   int32_t actions_i32;
   double win_reward, loss_reward, step_penalty;
+  const uint64_t* jump;  // [64][4] PCG64 jump-ahead table {A_hi, A_lo, C_hi, C_lo}, k = 1..64
+  uint64_t* diag;        // MS_DIAG builds only: per-env s_memtime stamps [n][8]
+  uint32_t dbg_flags;    // MS_DBG_* (msenv_debug.h)
 };
 
 // ---------------------------------------------------------------------------
@@ -79,19 +83,32 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
   return ((uint64_t)rfl((uint32_t)(x >> 32)) << 32) | rfl((uint32_t)x);
 }
 
-__device__ __forceinline__ uint64_t shfl_up1(uint64_t v, int lane) {   // lane r <- lane r-1
-  uint64_t o = __shfl_up(v, 1);
-  return lane == 0 ? 0ull : o;
+// DPP moves (gfx9 family): wave_shr:1 = lane r <- lane r-1, wave_shl:1 =
+// lane r <- lane r+1, row_shr:n = lane r <- lane r-n inside a 16-lane row;
+// bound_ctrl fills out-of-range sources with 0. One VALU op each, no LDS.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, true);
 }
-__device__ __forceinline__ uint64_t shfl_dn1(uint64_t v, int lane) {   // lane r <- lane r+1
-  uint64_t o = __shfl_down(v, 1);
-  return lane == kWave - 1 ? 0ull : o;
+__device__ __forceinline__ uint64_t wave_shr1(uint64_t v) {  // lane r <- lane r-1 (lane 0 <- 0)
+  return ((uint64_t)dpp32<0x138>((uint32_t)(v >> 32)) << 32) | dpp32<0x138>((uint32_t)v);
 }
-
+__device__ __forceinline__ uint64_t wave_shl1(uint64_t v) {  // lane r <- lane r+1 (lane 63 <- 0)
+  return ((uint64_t)dpp32<0x130>((uint32_t)(v >> 32)) << 32) | dpp32<0x130>((uint32_t)v);
+}
+__device__ __forceinline__ uint32_t readlane32(uint32_t v, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  return ((uint64_t)readlane32((uint32_t)(v >> 32), l) << 32) | readlane32((uint32_t)v, l);
+}
+// wave-wide sum: 4 DPP row-prefix adds + 4 readlanes (uniform result)
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  return v;
+  v += dpp32<0x111>(v);
+  v += dpp32<0x112>(v);
+  v += dpp32<0x114>(v);
+  v += dpp32<0x118>(v);
+  return readlane32(v, 15) + readlane32(v, 31) + readlane32(v, 47) + readlane32(v, 63);
 }
 
 // ---------------------------------------------------------------------------
@@ -284,8 +301,181 @@ __device__ __forceinline__ void stage_rows(uint64_t* sR, uint64_t* sM, uint64_t 
 }
 
 // ---------------------------------------------------------------------------
+// Mine placement (env.py:280-312): numpy's choice(allowed, K, replace=False)
+// = Floyd over j in [pop-K, pop) + (K-1) discarded Fisher-Yates draws.
+// ---------------------------------------------------------------------------
+struct Forbid {  // ascending forbidden cells (the click's clipped 3x3 block, or the click)
+  int f[9];
+  int m;
+  int pop;
+};
+
+template <int H_, int W_>
+__device__ __forceinline__ Forbid make_forbid(int cell, int ar, int ac, int K, bool guarantee, const Geo<H_, W_>& g) {
+  Forbid F;
+  F.m = 0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) F.f[i] = 0;
+  if (guarantee) {
+#pragma unroll
+    for (int dr = -1; dr <= 1; ++dr)
+#pragma unroll
+      for (int dc = -1; dc <= 1; ++dc) {
+        const int rr = ar + dr, cc = ac + dc;
+        if (rr >= 0 && rr < g.H && cc >= 0 && cc < g.W) {  // row-major scan = ascending cells
+#pragma unroll
+          for (int i = 0; i < 9; ++i)
+            if (i == F.m) F.f[i] = rr * g.W + cc;
+          ++F.m;
+        }
+      }
+  } else {
+    F.f[0] = cell;
+    F.m = 1;
+  }
+  F.pop = g.A() - F.m;
+  if (F.pop < K) {  // env.py:303-307: relax to the clicked cell only
+    F.f[0] = cell;
+    F.m = 1;
+    F.pop = g.A() - 1;
+  }
+  return F;
+}
+
+// One Floyd insertion in cell space; `mine` holds row r in lane r.
+template <int H_, int W_>
+__device__ __forceinline__ void floyd_insert(uint64_t& mine, int c1, int j, const Forbid& F, const Geo<H_, W_>& g,
+                                             int lane) {
+  int r1 = c1 / g.W;
+  int col = c1 - r1 * g.W;
+  if ((readlane64(mine, r1) >> col) & 1ull) {  // t already chosen: take j instead
+    c1 = map_allowed(j, F.f, F.m);
+    r1 = c1 / g.W;
+    col = c1 - r1 * g.W;
+  }
+  if (lane == r1) mine |= 1ull << col;
+}
+
+// Serial reference-order placement (also the fallback of the parallel one).
+template <int H_, int W_>
+__device__ void place_serial(Pcg& rng, uint64_t& mine, const Forbid& F, int K, const Geo<H_, W_>& g, int lane) {
+  mine = 0ull;
+  for (int j = F.pop - K; j < F.pop; ++j) {
+    const int t = (int)pcg_bounded(rng, (uint32_t)j);
+    floyd_insert(mine, map_allowed(t, F.f, F.m), j, F, g, lane);
+  }
+  for (int i = K - 1; i >= 1; --i) (void)pcg_bounded(rng, (uint32_t)i);  // shuffle draws
+}
+
+__device__ __forceinline__ bool lemire_rejects(uint32_t left, uint32_t bound) {
+  // numpy buffered_bounded_lemire_uint32: redraw iff leftover < (2^32-1-rng) % (rng+1)
+  const uint32_t excl = bound + 1u;
+  if (left >= excl) return false;
+  return left < (0xffffffffu - bound) % excl;
+}
+
+// Parallel placement: the PCG64 outputs the placement consumes are computed
+// lane-parallel by jump-ahead (state after k steps = A_k*s + C_k*inc, table
+// `jt` for k = 1..64), every draw's Floyd value / Lemire test is evaluated in
+// its lane, and only the set-membership chain of Floyd stays serial (one
+// readlane test per draw). Returns false, leaving rng/mine untouched, if any
+// consumed draw would be rejected by Lemire (p ~ 1e-6): the caller then runs
+// place_serial, so results are always the reference's.
+template <int H_, int W_>
+__device__ bool place_parallel(Pcg& rng, uint64_t& mine_out, const Forbid& F, int K, const uint64_t* __restrict__ jt,
+                               const Geo<H_, W_>& g, int lane) {
+  if (K == 0) {
+    mine_out = 0ull;
+    return true;
+  }
+  const int pop = F.pop;
+  const int z0 = (pop == K) ? 1 : 0;  // Floyd j = 0 consumes no draw
+  const int nF = K - z0;               // Floyd draws
+  const int D = nF + (K - 1);          // + shuffle draws
+  const int h0 = rng.has32 ? 1 : 0;    // draw 0 comes from the buffered half-word
+  const int rem = D - h0;              // draws taken from fresh outputs (>= 0: D >= 1 when h0)
+  const int n_out = (rem + 1) >> 1;
+  uint64_t mine = 0ull;
+  // Floyd iterations without a draw (only j = 0)
+  for (int i = 0; i < z0; ++i) floyd_insert(mine, map_allowed(0, F.f, F.m), pop - K + i, F, g, lane);
+  if (h0 && D > 0) {
+    const uint32_t bound = (nF > 0) ? (uint32_t)(pop - K + z0) : (uint32_t)(K - 1);
+    const uint64_t m64 = (uint64_t)rng.uinteger * (bound + 1u);
+    if (lemire_rejects((uint32_t)m64, bound)) return false;
+    if (nF > 0) floyd_insert(mine, map_allowed((int)(m64 >> 32), F.f, F.m), pop - K + z0, F, g, lane);
+  }
+  uint64_t bhi = rng.hi, blo = rng.lo;  // base state of the current chunk
+  uint64_t fin_hi = rng.hi, fin_lo = rng.lo;
+  uint32_t fin_uint = rng.uinteger;
+  const uint64_t* e = jt + 4 * lane;
+  const uint64_t Ah = e[0], Al = e[1], Ch = e[2], Cl = e[3];
+  // C_k * inc is the same for every chunk
+  const uint64_t ci_lo = Cl * rng.ilo;
+  const uint64_t ci_hi = __umul64hi(Cl, rng.ilo) + Cl * rng.ihi + Ch * rng.ilo;
+  for (int c = 0; 64 * c < n_out; ++c) {
+    const int q = 64 * c + lane + 1;  // this lane's output index (1-based)
+    const uint64_t l1 = Al * blo;
+    const uint64_t h1 = __umul64hi(Al, blo) + Al * bhi + Ah * blo;
+    const uint64_t sl = l1 + ci_lo;
+    const uint64_t sh = h1 + ci_hi + (sl < l1 ? 1ull : 0ull);
+    const uint64_t v = sh ^ sl;
+    const unsigned rot = (unsigned)(sh >> 58);
+    const uint64_t x = (v >> rot) | (v << ((64u - rot) & 63u));
+    int tc[2];
+    bool rej = false;
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int pidx = h0 + 2 * (q - 1) + hf;
+      const uint32_t d = hf ? (uint32_t)(x >> 32) : (uint32_t)x;
+      const bool is_floyd = pidx < nF;
+      const uint32_t bound = is_floyd ? (uint32_t)(pop - K + z0 + pidx) : (uint32_t)(K - 1 - (pidx - nF));
+      const uint64_t m64 = (uint64_t)d * (bound + 1u);
+      if (q <= n_out && pidx < D) rej |= lemire_rejects((uint32_t)m64, bound);
+      tc[hf] = is_floyd ? map_allowed((int)(m64 >> 32), F.f, F.m) : 0;
+    }
+    if (__ballot(rej) != 0ull) return false;
+    // serial Floyd chain over this chunk's draws
+    const int pbeg = h0 + 128 * c;
+    const int pend = min(h0 + 128 * c + 128, nF);
+    for (int pidx = pbeg; pidx < pend; ++pidx) {
+      const int rel = pidx - pbeg;
+      const int ln = rel >> 1;
+      const int c1 = (rel & 1) ? (int)readlane32((uint32_t)tc[1], ln) : (int)readlane32((uint32_t)tc[0], ln);
+      floyd_insert(mine, c1, pop - K + z0 + pidx, F, g, lane);
+    }
+    const int last = min(n_out - 64 * c, 64) - 1;  // lane holding this chunk's last output
+    fin_hi = readlane64(sh, last);
+    fin_lo = readlane64(sl, last);
+    fin_uint = readlane32((uint32_t)(x >> 32), last);
+    bhi = readlane64(sh, 63);
+    blo = readlane64(sl, 63);
+  }
+  rng.hi = fin_hi;
+  rng.lo = fin_lo;
+  if (D > 0) {
+    rng.has32 = (uint32_t)(rem & 1);
+    rng.uinteger = fin_uint;
+  }
+  mine_out = mine;
+  return true;
+}
+
+// ---------------------------------------------------------------------------
 // ms_step: one wave = one env.
 // ---------------------------------------------------------------------------
+#ifdef MS_DIAG
+#define STAMP(k)                                                              \
+  do {                                                                        \
+    if (p.diag && lane == 0) {                                                \
+      p.diag[env * 8 + (k)] = __builtin_amdgcn_s_memtime();                   \
+      if ((k) == 0) p.diag[env * 8 + 6] = __builtin_amdgcn_s_memrealtime();   \
+      if ((k) == 5) p.diag[env * 8 + 7] = __builtin_amdgcn_s_memrealtime();   \
+    }                                                                         \
+  } while (0)
+#else
+#define STAMP(k) do { } while (0)
+#endif
+
 template <int H_, int W_>
 __global__ __launch_bounds__(64) void k_step(KParams p) {
   __shared__ uint64_t sR[kWave];
@@ -293,11 +483,19 @@ __global__ __launch_bounds__(64) void k_step(KParams p) {
   const int lane = lane_id();
   const int64_t env = (int64_t)blockIdx.x;
   if (env >= p.n) return;
+  STAMP(0);
   const Geo<H_, W_> g(p.H, p.W);
   const int H = g.H, W = g.W, A = g.A(), NW = g.NW();
   const uint64_t rowmask = g.rowmask();
 
   EnvMeta* mp = p.meta + env;
+  uint64_t* mwords = p.mine_words + env * NW;
+  uint64_t* rwords = p.rev_words + env * NW;
+  // issue every load up front
+  uint64_t mine = load_row(mwords, g, lane);
+  uint64_t rev = load_row(rwords, g, lane);
+  int64_t a = p.actions_i32 ? (int64_t)reinterpret_cast<const int32_t*>(p.actions)[env]
+                            : reinterpret_cast<const int64_t*>(p.actions)[env];
   Pcg rng;
   rng.hi = rfl64(mp->st_hi);
   rng.lo = rfl64(mp->st_lo);
@@ -307,19 +505,12 @@ __global__ __launch_bounds__(64) void k_step(KParams p) {
   rng.uinteger = rfl(mp->uinteger);
   int32_t step_count = (int32_t)rfl((uint32_t)mp->step_count);
   bool fc = (rfl(mp->flags) & 1u) != 0;
-
-  int64_t a = p.actions_i32 ? (int64_t)reinterpret_cast<const int32_t*>(p.actions)[env]
-                            : reinterpret_cast<const int64_t*>(p.actions)[env];
   a = (int64_t)rfl64((uint64_t)a);
   int64_t cell64 = a % A;  // Python modulo (env.py:106)
   if (cell64 < 0) cell64 += A;
   const int cell = (int)cell64;
   const int ar = cell / W, ac = cell - (cell / W) * W;
-
-  uint64_t* mwords = p.mine_words + env * NW;
-  uint64_t* rwords = p.rev_words + env * NW;
-  uint64_t mine = load_row(mwords, g, lane);
-  uint64_t rev = load_row(rwords, g, lane);
+  STAMP(1);
 
   double reward = 0.0;
   bool done = false;
@@ -327,56 +518,17 @@ __global__ __launch_bounds__(64) void k_step(KParams p) {
   uint32_t newly = 0;
   bool mines_changed = false;
 
-  const bool cell_rev = __ballot(lane == ar && ((rev >> ac) & 1ull)) != 0ull;
+  const bool cell_rev = (readlane64(rev, ar) >> ac) & 1ull;
   if (!cell_rev) {
     if (!fc) {
-      // ---- _place_mines_safe (env.py:280-312) ----
-      int f[9];
-      int m = 0;
-#pragma unroll
-      for (int i = 0; i < 9; ++i) f[i] = 0;
-      if (p.guarantee) {
-#pragma unroll
-        for (int dr = -1; dr <= 1; ++dr)
-#pragma unroll
-          for (int dc = -1; dc <= 1; ++dc) {
-            const int rr = ar + dr, cc = ac + dc;
-            const bool in = rr >= 0 && rr < H && cc >= 0 && cc < W;
-            const int slot = (dr + 1) * 3 + (dc + 1);
-            // compact in ascending order: slot order is row-major = ascending cells
-            (void)slot;
-            if (in) {
-#pragma unroll
-              for (int i = 0; i < 9; ++i)
-                if (i == m) f[i] = rr * W + cc;
-              ++m;
-            }
-          }
-      } else {
-        f[0] = cell;
-        m = 1;
-      }
-      int pop = A - m;
-      if (pop < p.K) {  // env.py:303-307
-        f[0] = cell;
-        m = 1;
-        pop = A - 1;
-      }
-      mine = 0ull;
-      for (int j = pop - p.K; j < pop; ++j) {
-        const int t = (int)pcg_bounded(rng, (uint32_t)j);
-        int c1 = map_allowed(t, f, m);
-        const int r1 = c1 / W, col1 = c1 - (c1 / W) * W;
-        const bool taken = __ballot(lane == r1 && ((mine >> col1) & 1ull)) != 0ull;
-        if (taken) c1 = map_allowed(j, f, m);
-        const int r2 = c1 / W, col2 = c1 - (c1 / W) * W;
-        if (lane == r2) mine |= 1ull << col2;
-      }
-      for (int i = p.K - 1; i >= 1; --i) (void)pcg_bounded(rng, (uint32_t)i);  // shuffle draws
+      const Forbid F = make_forbid(cell, ar, ac, p.K, p.guarantee != 0, g);
+      if ((p.dbg_flags & MS_DBG_FORCE_SERIAL_PLACEMENT) || !place_parallel(rng, mine, F, p.K, p.jump, g, lane))
+        place_serial(rng, mine, F, p.K, g, lane);
       fc = true;
       mines_changed = true;
     }
-    const bool hit = __ballot(lane == ar && ((mine >> ac) & 1ull)) != 0ull;
+    STAMP(2);
+    const bool hit = (readlane64(mine, ar) >> ac) & 1ull;
     if (hit) {
       if (lane == ar) rev |= 1ull << ac;
       done = true;
@@ -384,26 +536,29 @@ __global__ __launch_bounds__(64) void k_step(KParams p) {
       reward += p.loss_reward;
     } else {
       // ---- flood_fill_reveal (env_numba.py:17-77) as dilation to fixpoint ----
-      const uint64_t up = shfl_up1(mine, lane), dn = shfl_dn1(mine, lane);
-      const uint64_t U = up | dn;
+      const uint64_t U = wave_shr1(mine) | wave_shl1(mine);
       const uint64_t nb = U | (U << 1) | (U >> 1) | (mine << 1) | (mine >> 1);
       const uint64_t zero = ~nb & rowmask;
       const uint64_t allow = ~mine & ~rev & (lane < H ? rowmask : 0ull);
-      uint64_t F = (lane == ar) ? (1ull << ac) : 0ull;
+      uint64_t Fr = (lane == ar) ? (1ull << ac) : 0ull;
       while (true) {
-        const uint64_t S = F & zero;
-        const uint64_t D = S | (S << 1) | (S >> 1);
-        const uint64_t Dv = D | shfl_up1(D, lane) | shfl_dn1(D, lane);
-        const uint64_t Fn = F | (Dv & allow);
-        const bool changed = __ballot(Fn != F) != 0ull;
-        F = Fn;
+        const uint64_t S = Fr & zero;
+        const uint64_t Dh = S | (S << 1) | (S >> 1);
+        const uint64_t Dv = Dh | wave_shr1(Dh) | wave_shl1(Dh);
+        const uint64_t Fn = Fr | (Dv & allow);
+        const bool changed = __ballot(Fn != Fr) != 0ull;
+        Fr = Fn;
         if (!changed) break;
       }
-      rev |= F;
-      newly = wave_sum((uint32_t)__popcll(F));
+      rev |= Fr;
+      newly = (uint32_t)__popcll(Fr);
     }
   }
-  const uint32_t total_rev = wave_sum((uint32_t)__popcll(rev));
+  STAMP(3);
+  // one reduction for both counts: total revealed (hi 16) | newly revealed (lo 16)
+  const uint32_t packed = wave_sum(((uint32_t)__popcll(rev) << 16) | newly);
+  const uint32_t total_rev = packed >> 16;
+  newly = packed & 0xffffu;
   if (!cell_rev && outcome != MS_OUTCOME_LOSS && (int)total_rev >= A - p.K) {
     done = true;
     outcome = MS_OUTCOME_WIN;
@@ -439,6 +594,7 @@ __global__ __launch_bounds__(64) void k_step(KParams p) {
   }
   if (mines_changed) store_rows(mwords, mine, sR, g, lane);
   store_rows(rwords, rev, sR, g, lane);
+  STAMP(4);
 
   // ---- observation + action mask (env.py:172-196) ----
   if (p.obs || p.mask) {
@@ -446,6 +602,7 @@ __global__ __launch_bounds__(64) void k_step(KParams p) {
     emit_obs(p.obs ? p.obs + env * 10 * A : nullptr, p.mask ? p.mask + env * A : nullptr, sR, sM,
              fc, g, lane);
   }
+  STAMP(5);
 }
 
 // ---------------------------------------------------------------------------
@@ -795,6 +952,9 @@ struct ms_handle {
   EnvMeta* meta;
   uint64_t* mine_words;
   uint64_t* rev_words;
+  uint64_t* jump;  // [64][4] PCG64 jump-ahead table (device)
+  uint64_t* diag;  // optional stamp buffer (MS_DIAG builds)
+  uint32_t dbg_flags;
 };
 
 namespace {
@@ -835,6 +995,9 @@ int do_step(ms_handle* h, const void* actions, int i32, float* obs, uint8_t* mas
   p.win_reward = h->cfg.win_reward;
   p.loss_reward = h->cfg.loss_reward;
   p.step_penalty = h->cfg.step_penalty;
+  p.jump = h->jump;
+  p.diag = h->diag;
+  p.dbg_flags = h->dbg_flags;
   hipStream_t s = (hipStream_t)stream;
   if (h->H == 16 && h->W == 16) launch_step<16, 16>(p, s);
   else if (h->H == 9 && h->W == 9) launch_step<9, 9>(p, s);
@@ -896,7 +1059,23 @@ int ms_create(const ms_cfg* cfg, int64_t n_total, uint64_t base_seed, int64_t en
     m.step_count = 0;
     m.flags = 0;
   }
+  // PCG64 jump-ahead: state after k steps = M^k s + (sum_{i<k} M^i) inc, k = 1..64
+  uint64_t jt[64 * 4];
+  {
+    const unsigned __int128 M = ((unsigned __int128)0x2360ED051FC65DA4ull << 64) | 0x4385DF649FCCF645ull;
+    unsigned __int128 Ak = 1, Ck = 0;
+    for (int k = 1; k <= 64; ++k) {
+      Ck = Ck + Ak;  // sum_{i<k} M^i
+      Ak = Ak * M;   // M^k
+      jt[4 * (k - 1) + 0] = (uint64_t)(Ak >> 64);
+      jt[4 * (k - 1) + 1] = (uint64_t)Ak;
+      jt[4 * (k - 1) + 2] = (uint64_t)(Ck >> 64);
+      jt[4 * (k - 1) + 3] = (uint64_t)Ck;
+    }
+  }
   hipError_t e = hipMalloc((void**)&h->meta, sizeof(EnvMeta) * (size_t)env_count);
+  if (e == hipSuccess) e = hipMalloc((void**)&h->jump, sizeof(jt));
+  if (e == hipSuccess) e = hipMemcpy(h->jump, jt, sizeof(jt), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc((void**)&h->mine_words, sizeof(uint64_t) * (size_t)env_count * h->NW);
   if (e == hipSuccess) e = hipMalloc((void**)&h->rev_words, sizeof(uint64_t) * (size_t)env_count * h->NW);
   if (e == hipSuccess)
@@ -918,7 +1097,22 @@ int ms_destroy(ms_handle* h) {
   if (h->meta) (void)hipFree(h->meta);
   if (h->mine_words) (void)hipFree(h->mine_words);
   if (h->rev_words) (void)hipFree(h->rev_words);
+  if (h->jump) (void)hipFree(h->jump);
   delete h;
+  return MS_OK;
+}
+
+// Diagnostics (not part of msenv.h): per-env s_memtime stamps [env_count][8]
+// are written by libmsenv_diag.so (built with -DMS_DIAG); NULL disables.
+int ms_set_debug_flags(ms_handle* h, uint32_t flags) {
+  if (!h) return fail(MS_EINVAL, "ms_set_debug_flags: null handle");
+  h->dbg_flags = flags;
+  return MS_OK;
+}
+
+int ms_set_diag(ms_handle* h, uint64_t* stamps) {
+  if (!h) return fail(MS_EINVAL, "ms_set_diag: null handle");
+  h->diag = stamps;
   return MS_OK;
 }
 

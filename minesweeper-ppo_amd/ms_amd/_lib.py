@@ -15,7 +15,8 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libmsenv.so")
+# MSENV_LIB may point at libmsenv_diag.so (tools/diag_step.py); default is the product build
+LIB_PATH = os.environ.get("MSENV_LIB") or os.path.join(PKG_DIR, "libmsenv.so")
 ABI_VERSION = 1
 
 MS_OUTCOME_NONE, MS_OUTCOME_WIN, MS_OUTCOME_LOSS = 0, 1, 2
@@ -51,7 +52,11 @@ SIGNATURES = {
     "ms_tape_actions": [_vp, _u64, _i32, _vp, _vp],
     "ms_gae": [_vp, _vp, _vp, _vp, _i32, _i64, _f32, _f32, _vp, _vp, _vp],
     "ms_sample_masked": [_vp, _vp, _i64, _i32, _u64, _u64, _vp, _vp, _vp],
+    # msenv_debug.h
+    "ms_set_debug_flags": [_vp, ctypes.c_uint32],
+    "ms_set_diag": [_vp, _vp],
 }
+MS_DBG_FORCE_SERIAL_PLACEMENT = 1
 _RESTYPES = {"ms_last_error": ctypes.c_char_p, "ms_abi_version": ctypes.c_int32}
 
 

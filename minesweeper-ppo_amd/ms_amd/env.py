@@ -291,6 +291,10 @@ class VecMinesweeper:
             L.check(self._lib.ms_tape_actions(self._h, int(t), int(mode), L.ptr(out), self._stream()))
         return out
 
+    def set_debug_flags(self, flags: int) -> None:
+        """msenv_debug.h hooks (tests): e.g. L.MS_DBG_FORCE_SERIAL_PLACEMENT."""
+        L.check(self._lib.ms_set_debug_flags(self._h, int(flags)))
+
     def rng_state(self) -> np.ndarray:
         out = torch.empty((self.num_envs, 6), dtype=torch.int64, device=self.device)
         with torch.cuda.device(self.device):

@@ -10,11 +10,11 @@ import pytest
 
 from conftest import ROOT
 
-HEADER = os.path.join(ROOT, "include", "msenv.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("msenv.h", "msenv_debug.h")]
 
 
 def header_functions():
-    src = open(HEADER).read()
+    src = "".join(open(h).read() for h in HEADERS)
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(ms_[a-z0-9_]+)\s*\(", src)))
 

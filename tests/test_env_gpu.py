@@ -185,3 +185,20 @@ def test_numpy_compat_mode(gpu):
     e = v.envs[3]
     assert e.first_click_done and e.revealed.shape == (9, 9) and e.mine_mask.sum() == 10
     assert (e.adjacent_counts <= 8).all() and not e.flags.any()
+
+
+@pytest.mark.parametrize("H,W,K", [(16, 16, 40), (30, 16, 99), (64, 62, 2000), (9, 9, 10), (4, 4, 15)])
+def test_parallel_and_serial_placement_agree(gpu, H, W, K):
+    """The lane-parallel PCG/Floyd placement and the serial reference-order
+    path (its fallback, forced here) give identical boards and RNG states."""
+    from ms_amd import _lib as L
+    a, b = _vec(H, W, K, 256, seed=21), _vec(H, W, K, 256, seed=21)
+    b.set_debug_flags(L.MS_DBG_FORCE_SERIAL_PLACEMENT)
+    a.reset()
+    b.reset()
+    for t in range(40):
+        act = a.tape_actions(t, 0)
+        ba, ra, da, _ = a.step(act)
+        bb, rb, db, _ = b.step(act)
+        assert torch.equal(ba["obs"], bb["obs"]) and torch.equal(ra, rb) and torch.equal(da, db), t
+        assert np.array_equal(a.rng_state(), b.rng_state()), t

@@ -1,0 +1,56 @@
+"""Diagnostic: per-phase in-kernel cycle stamps of k_step (libmsenv_diag.so).
+
+Phases (stamps 0..5): 0->1 loads, 1->2 placement, 2->3 flood fill,
+3->4 reduce+aux+state store, 4->5 obs/mask emit. Stamps 6/7 = s_memrealtime
+(100 MHz, chip-wide) at wave start/end, for the launch spread.
+Run: python tools/diag_step.py [--envs N] [--board 16x16x40] [--tape 0]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["MSENV_LIB"] = os.path.join(ROOT, "minesweeper-ppo_amd", "libmsenv_diag.so")
+sys.path.insert(0, os.path.join(ROOT, "minesweeper-ppo_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--envs", type=int, default=4096)
+ap.add_argument("--board", default="16x16x40")
+ap.add_argument("--tape", type=int, default=0)
+ap.add_argument("--steps", type=int, default=20)
+args = ap.parse_args()
+H, W, K = (int(x) for x in args.board.split("x"))
+from ms_amd import EnvConfig, VecMinesweeper, _lib as L  # noqa: E402
+
+v = VecMinesweeper(args.envs, EnvConfig(H=H, W=W, mine_count=K), seed=0)
+stamps = torch.zeros((args.envs, 8), dtype=torch.int64, device="cuda")
+v.reset()
+for t in range(30):
+    v.step(v.tape_actions(t, args.tape))
+L.check(v._lib.ms_set_diag(v._h, stamps.data_ptr()))
+rows = []
+for t in range(30, 30 + args.steps):
+    a = v.tape_actions(t, args.tape)
+    torch.cuda.synchronize()
+    v.step(a)
+    torch.cuda.synchronize()
+    rows.append(stamps.cpu().numpy().copy())
+S = np.concatenate(rows)
+ph = np.diff(S[:, :6], axis=1).astype(np.float64)
+names = ["loads", "placement", "flood", "reduce+store", "obs"]
+print(f"board {args.board} envs {args.envs} tape {args.tape}: cycles per phase (s_memtime ticks)")
+for i, n in enumerate(names):
+    col = ph[:, i]
+    print(f"  {n:14s} mean {col.mean():9.0f}  p50 {np.median(col):9.0f}  p99 {np.percentile(col, 99):9.0f}  max {col.max():9.0f}")
+tot = S[:, 5] - S[:, 0]
+print(f"  {'total':14s} mean {tot.mean():9.0f}  p50 {np.median(tot):9.0f}  p99 {np.percentile(tot, 99):9.0f}  max {tot.max():9.0f}")
+# realtime (100 MHz): spread of wave starts/ends within one launch
+for k in range(args.steps):
+    blk = rows[k]
+    st, en = blk[:, 6], blk[:, 7]
+    if k < 3:
+        print(f"  step {k}: wave start spread {(st.max()-st.min())/100:.2f} us, end spread "
+              f"{(en.max()-st.min())/100:.2f} us (first start -> last end), mean wave "
+              f"{(en-st).mean()/100:.2f} us")

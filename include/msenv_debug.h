@@ -14,7 +14,8 @@ extern "C" {
 #endif
 
 /* debug flags */
-#define MS_DBG_FORCE_SERIAL_PLACEMENT 1u /* skip the lane-parallel PCG/Floyd path */
+#define MS_DBG_FORCE_SERIAL_PLACEMENT 1u /* serial reference-order PCG draws + Floyd chain */
+#define MS_DBG_FORCE_CHAIN_PLACEMENT 2u  /* jump-ahead draws + serial Floyd chain (K > 128 path) */
 
 int ms_set_debug_flags(ms_handle* h, uint32_t flags);
 

@@ -382,7 +382,7 @@ __device__ __forceinline__ bool lemire_rejects(uint32_t left, uint32_t bound) {
 // consumed draw would be rejected by Lemire (p ~ 1e-6): the caller then runs
 // place_serial, so results are always the reference's.
 template <int H_, int W_>
-__device__ bool place_parallel(Pcg& rng, uint64_t& mine_out, const Forbid& F, int K, const uint64_t* __restrict__ jt,
+__device__ bool place_parallel(Pcg& rng, uint64_t& mine_out, const Forbid& F, int K, const uint64_t (&J)[4],
                                const Geo<H_, W_>& g, int lane) {
   if (K == 0) {
     mine_out = 0ull;
@@ -407,8 +407,7 @@ __device__ bool place_parallel(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
   uint64_t bhi = rng.hi, blo = rng.lo;  // base state of the current chunk
   uint64_t fin_hi = rng.hi, fin_lo = rng.lo;
   uint32_t fin_uint = rng.uinteger;
-  const uint64_t* e = jt + 4 * lane;
-  const uint64_t Ah = e[0], Al = e[1], Ch = e[2], Cl = e[3];
+  const uint64_t Ah = J[0], Al = J[1], Ch = J[2], Cl = J[3];
   // C_k * inc is the same for every chunk
   const uint64_t ci_lo = Cl * rng.ilo;
   const uint64_t ci_hi = __umul64hi(Cl, rng.ilo) + Cl * rng.ihi + Ch * rng.ilo;
@@ -460,6 +459,138 @@ __device__ bool place_parallel(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
   return true;
 }
 
+// x = XSL-RR(state after k steps from (bhi,blo)), jump entry of this lane (k = lane+1)
+struct Out {
+  uint64_t sh, sl, x;
+};
+__device__ __forceinline__ Out jump_out(uint64_t bhi, uint64_t blo, uint64_t Ah, uint64_t Al, uint64_t ci_hi,
+                                        uint64_t ci_lo) {
+  Out o;
+  const uint64_t l1 = Al * blo;
+  const uint64_t h1 = __umul64hi(Al, blo) + Al * bhi + Ah * blo;
+  o.sl = l1 + ci_lo;
+  o.sh = h1 + ci_hi + (o.sl < l1 ? 1ull : 0ull);
+  const uint64_t v = o.sh ^ o.sl;
+  const unsigned rot = (unsigned)(o.sh >> 58);
+  o.x = (v >> rot) | (v << ((64u - rot) & 63u));
+  return o;
+}
+
+__device__ __forceinline__ uint32_t bperm(uint32_t v, int src_lane) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
+}
+
+// Fully lane-parallel placement for 1 <= K <= 128 (every benchmark board):
+// the <= 128 PCG64 outputs come from two jump-ahead chunks, lane i (and i+64)
+// owns Floyd iteration i, and Floyd's sequential "t already chosen -> take j"
+// rule is solved as a fixpoint: sel_i = c_i unless some earlier sel equals
+// c_i, iterated until nothing changes (the sequential answer is the unique
+// fixpoint; collision chains are short, ~2-4 rounds). Set membership uses a
+// round-tagged LDS table indexed by cell. Returns false on a Lemire rejection
+// (caller falls back to place_serial), leaving rng untouched.
+template <int H_, int W_>
+__device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, int K, const uint64_t (&J)[4],
+                               uint32_t* tab, uint64_t* srow, const Geo<H_, W_>& g, int lane) {
+  const int A = g.A(), W = g.W;
+  const int pop = F.pop;
+  const int z0 = (pop == K) ? 1 : 0;
+  const int nF = K - z0;
+  const int D = nF + (K - 1);
+  const int h0 = rng.has32 ? 1 : 0;
+  const int rem = D - h0;
+  const int n_out = (rem + 1) >> 1;  // <= 128
+  const uint64_t ci_lo = J[3] * rng.ilo;
+  const uint64_t ci_hi = __umul64hi(J[3], rng.ilo) + J[3] * rng.ihi + J[2] * rng.ilo;
+  const Out o0 = jump_out(rng.hi, rng.lo, J[0], J[1], ci_hi, ci_lo);
+  Out o1 = o0;
+  if (n_out > 64) o1 = jump_out(readlane64(o0.sh, 63), readlane64(o0.sl, 63), J[0], J[1], ci_hi, ci_lo);
+  // Lemire rejection test of every consumed draw (draw p of output q, half hf)
+  bool rej = false;
+  if (h0 && D > 0) {
+    const uint32_t bound = (nF > 0) ? (uint32_t)(pop - K + z0) : (uint32_t)(K - 1);
+    rej |= lemire_rejects((uint32_t)((uint64_t)rng.uinteger * (bound + 1u)), bound);
+  }
+#pragma unroll
+  for (int ch = 0; ch < 2; ++ch) {
+    const uint64_t x = ch ? o1.x : o0.x;
+    const int q = 64 * ch + lane + 1;
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int pidx = h0 + 2 * (q - 1) + hf;
+      if (q <= n_out && pidx < D) {
+        const uint32_t d = hf ? (uint32_t)(x >> 32) : (uint32_t)x;
+        const uint32_t bound = pidx < nF ? (uint32_t)(pop - K + z0 + pidx) : (uint32_t)(K - 1 - (pidx - nF));
+        rej |= lemire_rejects((uint32_t)((uint64_t)d * (bound + 1u)), bound);
+      }
+    }
+  }
+  if (__ballot(rej) != 0ull) return false;
+  // Floyd candidates: lane owns iterations i = lane + 64 s
+  int cand[2], alt[2], sel[2];
+  bool valid[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const int i = lane + 64 * s2;
+    valid[s2] = i < K;
+    const int j = pop - K + i;
+    const int pidx = i - z0;
+    const int idx = pidx - h0;
+    // ds_bpermute delivers the SOURCE lane's register: fetch both halves of both
+    // chunks in converged control flow, then select by this lane's idx
+    const int src = (idx >> 1) & 63;
+    const uint32_t w0l = bperm((uint32_t)o0.x, src), w0h = bperm((uint32_t)(o0.x >> 32), src);
+    const uint32_t w1l = bperm((uint32_t)o1.x, src), w1h = bperm((uint32_t)(o1.x >> 32), src);
+    uint32_t d = (idx >> 7) ? ((idx & 1) ? w1h : w1l) : ((idx & 1) ? w0h : w0l);
+    if (h0 && pidx == 0) d = rng.uinteger;
+    const uint32_t t = (i >= z0) ? (uint32_t)(((uint64_t)d * (uint32_t)(j + 1)) >> 32) : 0u;
+    cand[s2] = map_allowed((int)t, F.f, F.m);
+    alt[s2] = map_allowed(j, F.f, F.m);
+    sel[s2] = cand[s2];
+  }
+  for (int c = lane; c < A; c += kWave) tab[c] = 0u;
+  __syncthreads();
+  for (uint32_t round = 1; round <= (uint32_t)K + 1; ++round) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+      if (valid[s2]) atomicMax(&tab[sel[s2]], (round << 16) | (0xFFFFu - (uint32_t)(lane + 64 * s2)));
+    __syncthreads();
+    bool changed = false;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      if (valid[s2]) {
+        const uint32_t e = tab[cand[s2]];
+        const bool coll = (e >> 16) == round && (0xFFFFu - (e & 0xFFFFu)) < (uint32_t)(lane + 64 * s2);
+        const int nv = coll ? alt[s2] : cand[s2];
+        changed |= nv != sel[s2];
+        sel[s2] = nv;
+      }
+    }
+    __syncthreads();
+    if (__ballot(changed) == 0ull) break;
+  }
+  srow[lane] = 0ull;
+  __syncthreads();
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+    if (valid[s2]) {
+      const int r = sel[s2] / W;
+      atomicOr((unsigned long long*)&srow[r], 1ull << (sel[s2] - r * W));
+    }
+  __syncthreads();
+  mine_out = lane < g.H ? srow[lane] : 0ull;
+  __syncthreads();
+  // RNG state after the D draws
+  if (n_out > 0) {
+    const int lastq = n_out - 1;
+    const Out& ol = (lastq >= 64) ? o1 : o0;
+    rng.hi = readlane64(ol.sh, lastq & 63);
+    rng.lo = readlane64(ol.sl, lastq & 63);
+    rng.uinteger = readlane32((uint32_t)(ol.x >> 32), lastq & 63);
+  }
+  if (D > 0) rng.has32 = (uint32_t)(rem & 1);
+  return true;
+}
+
 // ---------------------------------------------------------------------------
 // ms_step: one wave = one env.
 // ---------------------------------------------------------------------------
@@ -480,10 +611,20 @@ template <int H_, int W_>
 __global__ __launch_bounds__(64) void k_step(KParams p) {
   __shared__ uint64_t sR[kWave];
   __shared__ uint64_t sM[kWave + 2];
+  __shared__ uint32_t sTab[(H_ && W_) ? H_ * W_ : kMaxH * kMaxW];
   const int lane = lane_id();
   const int64_t env = (int64_t)blockIdx.x;
   if (env >= p.n) return;
   STAMP(0);
+  // jump-ahead entry k = lane+1 (2 KiB shared by all waves: L2-resident), prefetched
+  uint64_t J[4];
+  {
+    const uint64_t* e = p.jump + 4 * lane;
+    J[0] = e[0];
+    J[1] = e[1];
+    J[2] = e[2];
+    J[3] = e[3];
+  }
   const Geo<H_, W_> g(p.H, p.W);
   const int H = g.H, W = g.W, A = g.A(), NW = g.NW();
   const uint64_t rowmask = g.rowmask();
@@ -522,8 +663,14 @@ __global__ __launch_bounds__(64) void k_step(KParams p) {
   if (!cell_rev) {
     if (!fc) {
       const Forbid F = make_forbid(cell, ar, ac, p.K, p.guarantee != 0, g);
-      if ((p.dbg_flags & MS_DBG_FORCE_SERIAL_PLACEMENT) || !place_parallel(rng, mine, F, p.K, p.jump, g, lane))
-        place_serial(rng, mine, F, p.K, g, lane);
+      bool ok = false;
+      if (!(p.dbg_flags & MS_DBG_FORCE_SERIAL_PLACEMENT)) {
+        if (p.K >= 1 && p.K <= 128 && !(p.dbg_flags & MS_DBG_FORCE_CHAIN_PLACEMENT))
+          ok = place_fixpoint(rng, mine, F, p.K, J, sTab, sR, g, lane);
+        else
+          ok = place_parallel(rng, mine, F, p.K, J, g, lane);
+      }
+      if (!ok) place_serial(rng, mine, F, p.K, g, lane);
       fc = true;
       mines_changed = true;
     }

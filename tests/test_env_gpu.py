@@ -202,3 +202,28 @@ def test_parallel_and_serial_placement_agree(gpu, H, W, K):
         bb, rb, db, _ = b.step(act)
         assert torch.equal(ba["obs"], bb["obs"]) and torch.equal(ra, rb) and torch.equal(da, db), t
         assert np.array_equal(a.rng_state(), b.rng_state()), t
+
+
+@pytest.mark.parametrize("H,W,K", [(16, 16, 40), (30, 16, 99), (16, 30, 128), (9, 9, 10), (4, 4, 15),
+                                   (12, 12, 129), (3, 3, 8)])
+def test_fixpoint_chain_and_serial_placement_agree(gpu, H, W, K):
+    """All three placement paths (lane-parallel fixpoint K<=128, jump-ahead +
+    serial Floyd chain, fully serial reference order) agree with the oracle."""
+    from ms_amd import _lib as L
+    vs = [_vec(H, W, K, 192, seed=33) for _ in range(3)]
+    vs[1].set_debug_flags(2)  # MS_DBG_FORCE_CHAIN_PLACEMENT
+    vs[2].set_debug_flags(L.MS_DBG_FORCE_SERIAL_PLACEMENT)
+    o = O.OracleVec(H, W, K, 192, seed=33)
+    o.reset()
+    for v in vs:
+        v.reset()
+    for t in range(30):
+        act = vs[0].tape_actions(t, 0)
+        ref = o.step(act.cpu().numpy())
+        for v in vs:
+            b, r, d, _ = v.step(act)
+            assert np.array_equal(b["obs"].cpu().numpy(), ref["obs"]), t
+            assert np.array_equal(r.cpu().numpy(), ref["reward"]), t
+        st = o.rng_state()
+        for v in vs:
+            assert np.array_equal(v.rng_state(), st), t

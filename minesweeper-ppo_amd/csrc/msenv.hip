@@ -194,13 +194,27 @@ __device__ __forceinline__ uint64_t load_row(const uint64_t* words, const Geo<H_
   return (words[w] >> sh) & g.rowmask();
 }
 
-// rows -> packed words through LDS (srow: this wave's 64-entry row buffer).
+// rows -> packed words. rows-per-word a power of two (W=16: 4, W=30: 2, W=8: 8,
+// W>32: 1): OR the lane group's shifted rows with DPP (quad_perm xor1/xor2,
+// row_half_mirror, row_mirror), no LDS. Otherwise (W=9: 7 rows/word) through
+// LDS (srow: this wave's 64-entry row buffer).
 template <int H_, int W_>
 __device__ __forceinline__ void store_rows(uint64_t* words, uint64_t row, uint64_t* srow,
                                            const Geo<H_, W_>& g, int lane) {
+  const int nw = g.NW(), rpw = g.RPW();
+  if ((rpw & (rpw - 1)) == 0 && rpw <= 16) {
+    uint64_t v = row << ((lane & (rpw - 1)) * g.W);
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    if (rpw >= 2) { lo |= dpp32<0xB1>(lo); hi |= dpp32<0xB1>(hi); }
+    if (rpw >= 4) { lo |= dpp32<0x4E>(lo); hi |= dpp32<0x4E>(hi); }
+    if (rpw >= 8) { lo |= dpp32<0x141>(lo); hi |= dpp32<0x141>(hi); }
+    if (rpw >= 16) { lo |= dpp32<0x140>(lo); hi |= dpp32<0x140>(hi); }
+    const int w = lane / rpw;
+    if ((lane & (rpw - 1)) == 0 && w < nw) words[w] = ((uint64_t)hi << 32) | lo;
+    return;
+  }
   srow[lane] = row;
   __syncthreads();
-  const int nw = g.NW(), rpw = g.RPW();
   if (lane < nw) {
     uint64_t acc = 0;
     for (int k = 0; k < rpw; ++k) {
@@ -244,11 +258,23 @@ __device__ __forceinline__ void emit_obs(float* __restrict__ obs, uint8_t* __res
     const int nq = A >> 2;
     for (int q = lane; q < nq; q += kWave) {
       uint32_t code[4];
+      if ((W & 3) == 0) {  // the quad lies in one row: 4 LDS reads for 4 cells
+        const int r = (4 * q) / W, c0 = 4 * q - r * W;
+        const uint32_t rv = (uint32_t)(sR[r] >> c0);
+        const uint64_t up = sM[r] >> c0, mid = sM[r + 1] >> c0, dn = sM[r + 2] >> c0;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int i = 4 * q + k;
-        const int r = i / W, c = i - (i / W) * W;
-        code[k] = cell_code(sR, sM, r, c, fc);
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t cnt = (uint32_t)__popcll((up >> k) & 7ull) + (uint32_t)__popcll((dn >> k) & 7ull) +
+                               (uint32_t)((mid >> k) & 1ull) + (uint32_t)((mid >> (k + 2)) & 1ull);
+          code[k] = ((rv >> k) & 1u) ? (fc ? 1u + cnt : 10u) : 0u;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int i = 4 * q + k;
+          const int r = i / W, c = i - (i / W) * W;
+          code[k] = cell_code(sR, sM, r, c, fc);
+        }
       }
       if (obs) {
         float4* o4 = reinterpret_cast<float4*>(obs) + q;
@@ -616,15 +642,6 @@ __global__ __launch_bounds__(64) void k_step(KParams p) {
   const int64_t env = (int64_t)blockIdx.x;
   if (env >= p.n) return;
   STAMP(0);
-  // jump-ahead entry k = lane+1 (2 KiB shared by all waves: L2-resident), prefetched
-  uint64_t J[4];
-  {
-    const uint64_t* e = p.jump + 4 * lane;
-    J[0] = e[0];
-    J[1] = e[1];
-    J[2] = e[2];
-    J[3] = e[3];
-  }
   const Geo<H_, W_> g(p.H, p.W);
   const int H = g.H, W = g.W, A = g.A(), NW = g.NW();
   const uint64_t rowmask = g.rowmask();
@@ -646,6 +663,17 @@ __global__ __launch_bounds__(64) void k_step(KParams p) {
   rng.uinteger = rfl(mp->uinteger);
   int32_t step_count = (int32_t)rfl((uint32_t)mp->step_count);
   bool fc = (rfl(mp->flags) & 1u) != 0;
+  // jump-ahead entry k = lane+1 (2 KiB shared by every wave, L2-resident); only
+  // a board whose next click is its first needs it
+  uint64_t J[4] = {0ull, 0ull, 0ull, 0ull};
+  if (!fc) {
+    const ulonglong2* e = reinterpret_cast<const ulonglong2*>(p.jump + 4 * lane);
+    const ulonglong2 a0 = e[0], a1 = e[1];
+    J[0] = a0.x;
+    J[1] = a0.y;
+    J[2] = a1.x;
+    J[3] = a1.y;
+  }
   a = (int64_t)rfl64((uint64_t)a);
   int64_t cell64 = a % A;  // Python modulo (env.py:106)
   if (cell64 < 0) cell64 += A;

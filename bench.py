@@ -49,6 +49,10 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
     ap.add_argument("--diag-no-obs", action="store_true", help="diagnostic: skip obs/mask outputs")
     ap.add_argument("--graph", type=int, default=1, help="capture the timed steps in a HIP graph")
+    ap.add_argument("--ppo-updates", type=int, default=2,
+                    help="timed combined rollout+GAE+PPO updates (0 disables; +1 untimed warm-up)")
+    ap.add_argument("--ppo-steps-per-env", type=int, default=64)
+    ap.add_argument("--amp", default="bf16", choices=["bf16", "fp16", "fp32"])
     return ap.parse_args()
 
 
@@ -84,6 +88,55 @@ def cpu_baseline(H, W, K, n_envs, seed, tape, budget_s, threads):
     return dict(value=n_envs * steps / el, unit="env_steps/s", cores=threads, kind="port",
                 sample=f"{steps} steps x {n_envs} envs {H}x{W}x{K} (tape {tape}) in {el:.1f}s, "
                        f"oracle/ms_oracle.c on {threads} pthreads")
+
+
+# fwd / fwd+bwd GFLOP per 16x16 sample of the shipped model (torch flop counter)
+GFLOP_FWD_16, GFLOP_FWDBWD_16 = 0.4388, 1.3073
+BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16
+
+
+def ppo_bench(args, world, rank, local_rank, dev):
+    """Combined rollout + GAE + PPO-update loop (BASELINE metric, 2nd half):
+    configs/16x16x40_medium.yaml with num_envs = envs_per_gpu * world (global),
+    T = 64, 3 epochs x 8 minibatches, flat-gradient RCCL all-reduce per minibatch."""
+    from ms_amd.dist import DistInfo
+    from ms_amd.train import Trainer, load_config
+    cfg, env_d, model_d, extras = load_config(os.path.join(ROOT, "configs", "16x16x40_medium.yaml"))
+    cfg.num_envs = args.envs * world
+    cfg.steps_per_env = args.ppo_steps_per_env
+    cfg.total_updates = 4000
+    info = DistInfo(rank=rank, world=world, local_rank=local_rank,
+                    group=dist.group.WORLD if world > 1 else None)
+    tr = Trainer(cfg, env_d, model_d, extras, seed=args.seed, info=info, amp=args.amp, device=dev)
+    tr.update(0)  # warm-up: MIOpen kernel selection, allocator
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    prof = []
+    for u in range(args.ppo_updates):
+        prof.append(tr.update(1 + u, profile=True))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t[0])
+    spu = el / args.ppo_updates
+    n_loc, T = args.envs, cfg.steps_per_env
+    gflop = (T * n_loc * GFLOP_FWD_16 + n_loc * GFLOP_FWD_16 + cfg.ppo_epochs * T * n_loc * GFLOP_FWDBWD_16)
+    mean = lambda k: float(np.mean([p[k] for p in prof]))  # noqa: E731
+    return {"metric": "PPO updates/sec (combined rollout + GAE + 3x8 minibatch update)",
+            "updates_per_s": 1.0 / spu, "s_per_update": spu,
+            "samples_per_s": n_loc * world * T / spu, "envs_total": n_loc * world, "steps_per_env": T,
+            "rollout_s": mean("rollout_s"), "gae_s": mean("gae_s"), "ppo_s": mean("ppo_s"),
+            "amp": args.amp, "model": "cnn_residual 96ch x 5 blocks (950,947 params)",
+            "roofline": {"bound": "mfma", "achieved": gflop / spu / 1e3, "peak": BF16_DENSE_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": gflop / spu / 1e3 / BF16_DENSE_PEAK_TFLOPS,
+                         "traffic": None, "algo_gflop_per_update_per_gpu": gflop},
+            "loss": prof[-1].get("loss"), "entropy": prof[-1].get("entropy")}
 
 
 def main():
@@ -200,6 +253,8 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": "k_step", "kernel_ms": kern_ms, "algo_bytes_per_env_step": bpe},
     }
+    if args.ppo_updates > 0:
+        out["ppo"] = ppo_bench(args, world, rank, local_rank, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         out["cpu_baseline"] = cpu_baseline(H, W, K, n_local, args.seed, args.tape, args.cpu_seconds,

@@ -1,0 +1,286 @@
+"""Training driver — the MI355X counterpart of train_rl.py (reference
+train_rl.py:82-787), same YAML schema and CLI flags, one process per GPU.
+
+    python -m ms_amd.train --config configs/training/16x16x40_medium.yaml --updates 100
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m ms_amd.train --config ...
+
+Per update (train_rl.py:514-576): entropy / aux-weight schedules ->
+collect_rollout (on device) -> GAE (ms_gae) -> ppo_epochs x mini_batches
+ppo_update (bf16 autocast; RCCL flat-gradient all-reduce when world > 1) ->
+CosineAnnealingLR.step(). Checkpoints keep the reference payload
+{"model", "cfg", "model_meta"[, "metric"]} (train_rl.py:623-630, 715-721).
+``num_envs`` is GLOBAL: each rank steps num_envs / world envs of the global
+seed list, so the trajectories do not depend on the world size.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import json
+import logging
+import os
+import time
+from dataclasses import asdict, dataclass
+from typing import Dict
+
+import torch
+import yaml
+from torch.optim import AdamW
+from torch.optim.lr_scheduler import CosineAnnealingLR
+
+from .buffers import RolloutBuffer
+from .dist import DistInfo, broadcast_module, init_from_env
+from .env import EnvConfig, VecMinesweeper
+from .models import build_model, strip_compile_prefix
+from .ppo import FlatGrads, PPOConfig, ppo_update
+from .rollout import collect_rollout
+
+
+@dataclass
+class PPOTrainConfig:  # train_rl.py:82-107
+    H: int = 8
+    W: int = 8
+    mine_count: int = 10
+    guarantee_safe_neighborhood: bool = True
+    num_envs: int = 256
+    steps_per_env: int = 128
+    mini_batches: int = 8
+    ppo_epochs: int = 3
+    gamma: float = 0.995
+    gae_lambda: float = 0.95
+    clip_eps: float = 0.2
+    clip_eps_v: float = 0.2
+    vf_coef: float = 0.5
+    ent_coef: float = 0.003
+    ent_coef_min: float = 0.003
+    ent_decay_updates: int = 0
+    lr: float = 3e-4
+    max_grad_norm: float = 0.5
+    aux_mine_weight: float = 0.0
+    aux_mine_calib_weight: float = 0.0
+    total_updates: int = 1000
+
+
+def load_config(path: str | None):
+    """train_rl.py:110-143: (PPOTrainConfig, env dict, model dict, extras)."""
+    if path is None:
+        return PPOTrainConfig(), {}, {}, {}
+    with open(path) as f:
+        data = yaml.safe_load(f) or {}
+    env_d = data.get("env", {}) or {}
+    ppo_d = data.get("ppo", {}) or {}
+    model_d = data.get("model", {}) or {}
+    base = PPOTrainConfig()
+    kw = {}
+    for k in ("H", "W", "mine_count", "guarantee_safe_neighborhood"):
+        kw[k] = env_d.get(k, getattr(base, k))
+    for k in PPOTrainConfig.__dataclass_fields__:
+        if k not in kw:
+            kw[k] = ppo_d.get(k, getattr(base, k))
+    extras = {k: v for k, v in data.items() if k not in ("env", "ppo", "model")}
+    return PPOTrainConfig(**kw), env_d, model_d, extras
+
+
+def ent_coef_at(cfg: PPOTrainConfig, update: int) -> float:  # train_rl.py:515-523
+    if cfg.ent_decay_updates > 0:
+        frac = min(1.0, update / max(1, int(cfg.ent_decay_updates)))
+        return float(cfg.ent_coef + (cfg.ent_coef_min - cfg.ent_coef) * frac)
+    return float(cfg.ent_coef)
+
+
+def aux_weight_at(update: int, total: int, base: float, warm_w: float, final_w: float, warm_u: int,
+                  power: float) -> float:  # train_rl.py:526-541
+    if not (base > 0 or warm_w > 0 or final_w > 0):
+        return 0.0
+    if warm_u > 0 and (update + 1) <= warm_u:
+        w = warm_w
+    else:
+        frac = (update + 1 - warm_u) / max(1, total - warm_u) if total > warm_u else 1.0
+        frac = min(1.0, max(0.0, frac))
+        if power != 1.0:
+            frac = frac ** power
+        w = warm_w + (final_w - warm_w) * frac
+    return float(max(0.0, w))
+
+
+class Trainer:
+    """Holds env shard, model, optimizer and buffers; `update()` runs one PPO
+    update. Used by main() and by bench.py's combined-loop measurement."""
+
+    def __init__(self, cfg: PPOTrainConfig, env_d: Dict, model_d: Dict, extras: Dict, *, seed: int = 0,
+                 model_name: str | None = None, info: DistInfo | None = None, amp: str = "bf16",
+                 device: torch.device | None = None):
+        self.cfg = cfg
+        self.info = info or DistInfo()
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        training = extras.get("training", {}) if isinstance(extras, dict) else {}
+        training = training if isinstance(training, dict) else {}
+        rollout = training.get("rollout", {}) or {}
+        if "num_envs" in rollout:
+            cfg.num_envs = int(rollout["num_envs"])
+        if "steps_per_env" in rollout:
+            cfg.steps_per_env = int(rollout["steps_per_env"])
+        env_kwargs = {"H": cfg.H, "W": cfg.W, "mine_count": cfg.mine_count,
+                      "guarantee_safe_neighborhood": cfg.guarantee_safe_neighborhood}
+        env_kwargs.update(env_d)
+        env_kwargs.pop("include_frontier_channel", None)
+        self.env_cfg = EnvConfig(**env_kwargs)
+        late = training.get("late_start") if isinstance(training.get("late_start"), dict) else None
+        self.vec = VecMinesweeper(cfg.num_envs, self.env_cfg, seed=seed, late_start_cfg=late,
+                                  late_start_seed=seed + 1, device=self.device,
+                                  shard=(self.info.rank, self.info.world))
+        mcfg = dict(model_d)
+        self.model_name = model_name or mcfg.pop("name", "cnn")
+        mcfg.pop("name", None)
+        self.model_meta = {"name": self.model_name, "config": dict(mcfg)}
+        torch.manual_seed(seed)
+        self.model = build_model(self.model_name, obs_shape=(10, self.env_cfg.H, self.env_cfg.W),
+                                 model_cfg=mcfg).to(self.device)
+        broadcast_module(self.model, self.info)
+        self.opt = AdamW(self.model.parameters(), lr=cfg.lr)
+        self.sched = CosineAnnealingLR(self.opt, T_max=cfg.total_updates)
+        self.amp_dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": None}[amp]
+        self.scaler = torch.amp.GradScaler("cuda") if amp == "fp16" else None
+        self.flat = FlatGrads(self.model.parameters())
+        self.ppo_cfg = PPOConfig(clip_eps=cfg.clip_eps, clip_eps_v=cfg.clip_eps_v, vf_coef=cfg.vf_coef,
+                                 ent_coef=cfg.ent_coef, aux_mine_weight=cfg.aux_mine_weight,
+                                 aux_mine_calib_weight=cfg.aux_mine_calib_weight,
+                                 max_grad_norm=cfg.max_grad_norm,
+                                 beta_l2=float(training.get("beta_l2", 0.0)))
+        self.aux_base = float(cfg.aux_mine_weight)
+        self.aux_warm_w = float(training.get("aux_mine_warmup_weight", self.aux_base))
+        self.aux_final_w = float(training.get("aux_mine_final_weight", self.aux_base))
+        self.aux_warm_u = max(0, int(training.get("aux_mine_warmup_updates", 0)))
+        self.aux_power = max(1e-6, float(training.get("aux_mine_decay_power", 1.0)))
+        self.buffer: RolloutBuffer | None = None
+        self.seed = seed
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(seed * 1000003 + self.info.rank)
+
+    def update(self, update: int, profile: bool = False) -> Dict[str, float]:
+        """One PPO update. ``profile`` synchronises between phases and adds
+        rollout_s / gae_s / ppo_s wall times to the stats."""
+        cfg, pc = self.cfg, self.ppo_cfg
+        tick = [time.perf_counter()]
+
+        def mark():
+            if profile:
+                torch.cuda.synchronize(self.device)
+                tick.append(time.perf_counter())
+        pc.ent_coef = ent_coef_at(cfg, update)
+        pc.aux_mine_weight = aux_weight_at(update, cfg.total_updates, self.aux_base, self.aux_warm_w,
+                                           self.aux_final_w, self.aux_warm_u, self.aux_power)
+        self.model.train()
+        self.buffer, aux = collect_rollout(
+            self.vec, self.model, cfg.steps_per_env, self.device, pc.aux_mine_weight,
+            pc.aux_mine_calib_weight, amp_dtype=self.amp_dtype, buffer=self.buffer,
+            sample_seed=self.seed * 7919 + 17, sample_counter=(update << 20) + (self.info.rank << 40))
+        mark()
+        self.buffer.compute_gae(aux["last_values"], gamma=cfg.gamma, lam=cfg.gae_lambda)
+        mark()
+        B = self.vec.num_envs * cfg.steps_per_env
+        mb = B // cfg.mini_batches
+        acc: Dict[str, torch.Tensor] = {}
+        n = 0
+        group = self.info.group if self.info.world > 1 else None
+        for _ in range(cfg.ppo_epochs):
+            for batch in self.buffer.get_minibatches(mb, generator=self.gen):
+                st = ppo_update(self.model, self.opt, batch, pc, self.scaler, amp_dtype=self.amp_dtype,
+                                group=group, flat_grads=self.flat, sync_stats=False)
+                for k, v in st.items():
+                    acc[k] = acc[k] + v if k in acc else v
+                n += 1
+        self.sched.step()
+        keys = sorted(acc)
+        vals = torch.stack([acc[k] for k in keys]).div(max(1, n)).tolist() if keys else []
+        out = dict(zip(keys, vals))
+        out["aux_weight"] = pc.aux_mine_weight
+        out["ent_coef"] = pc.ent_coef
+        if profile:
+            mark()
+            out["rollout_s"], out["gae_s"], out["ppo_s"] = (tick[1] - tick[0], tick[2] - tick[1],
+                                                           tick[3] - tick[2])
+        return out
+
+    def checkpoint(self, path: str, metric=None) -> None:
+        payload = {"model": {k: v.detach().cpu() for k, v in self.model.state_dict().items()},
+                   "cfg": asdict(self.cfg), "model_meta": self.model_meta}
+        if metric is not None:
+            payload["metric"] = metric
+        torch.save(payload, path)
+
+    def load_init(self, path: str) -> None:  # train_rl.py:401-413 (weights only, strict=False)
+        state = torch.load(path, map_location=self.device, weights_only=True)
+        sd = state["model"] if isinstance(state, dict) and "model" in state else state
+        self.model.load_state_dict(strip_compile_prefix(sd), strict=False)
+        broadcast_module(self.model, self.info)
+
+
+def main(argv=None) -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=str, default=None)
+    ap.add_argument("--model", type=str, default=None)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--out", type=str, default="runs/ppo")
+    ap.add_argument("--updates", type=int, default=None)
+    ap.add_argument("--init_ckpt", type=str, default=None)
+    ap.add_argument("--save_every", type=int, default=50)
+    ap.add_argument("--amp", choices=["bf16", "fp16", "fp32"], default="bf16")
+    # accepted for CLI parity with train_rl.py:293-315 (evaluation is SURVEY.md §8f "next")
+    for flag in ("--eval_episodes", "--eval_num_envs", "--eval_quick_episodes", "--quick_eval_pairs",
+                 "--quick_eval_interval", "--eval_pairs"):
+        ap.add_argument(flag, type=int, default=None)
+    ap.add_argument("--skip_final_eval", action="store_true")
+    ap.add_argument("--grad_checkpoint", action="store_true")
+    ap.add_argument("--flash_attention", choices=["auto", "on", "off"], default="auto")
+    args = ap.parse_args(argv)
+
+    info = init_from_env()
+    cfg, env_d, model_d, extras = load_config(args.config)
+    if args.updates is not None:
+        cfg.total_updates = int(args.updates)
+    logging.basicConfig(level=logging.INFO if info.is_main else logging.WARNING,
+                        format="[%(asctime)s] %(message)s", datefmt="%H:%M:%S")
+    log = logging.getLogger("ms_amd.train")
+    device = torch.device("cuda", info.local_rank if info.world > 1 else torch.cuda.current_device())
+    torch.cuda.set_device(device)
+    tr = Trainer(cfg, env_d, model_d, extras, seed=args.seed, model_name=args.model, info=info, amp=args.amp,
+                 device=device)
+    if args.init_ckpt:
+        tr.load_init(args.init_ckpt)
+    if info.is_main:
+        os.makedirs(args.out, exist_ok=True)
+        n_params = sum(p.numel() for p in tr.model.parameters())
+        log.info(f"Model: {tr.model_name} | params={n_params / 1e6:.2f}M | world={info.world} | "
+                 f"envs/rank={tr.vec.num_envs}")
+    rows = []
+    for update in range(cfg.total_updates):
+        t0 = time.time()
+        st = tr.update(update)
+        dt = time.time() - t0
+        row = {"update": update + 1, "seconds": dt, "steps": cfg.num_envs * cfg.steps_per_env, **st}
+        rows.append(row)
+        if info.is_main:
+            extra = "".join(f" {k}={st[k]:.4f}" for k in ("aux_bce", "aux_calib") if k in st)
+            log.info(f"upd {update + 1}/{cfg.total_updates} | {dt:.2f}s | steps={row['steps']} | "
+                     f"pi={st.get('policy_loss', float('nan')):.4f} v={st.get('value_loss', float('nan')):.4f} "
+                     f"ent={st.get('entropy', float('nan')):.4f}{extra} ent_coef={st['ent_coef']:.4f}")
+            if (update + 1) % max(1, args.save_every) == 0:
+                tr.checkpoint(os.path.join(args.out, "ckpt_latest.pt"))
+    if info.is_main:
+        keys = sorted(set().union(*rows)) if rows else []
+        with open(os.path.join(args.out, "train_metrics.csv"), "w", newline="") as f:
+            w = csv.DictWriter(f, fieldnames=keys)
+            w.writeheader()
+            for r in rows:
+                w.writerow(r)
+        tr.checkpoint(os.path.join(args.out, "ckpt_final.pt"))
+        with open(os.path.join(args.out, "summary.json"), "w") as f:
+            json.dump({"checkpoint": "ckpt_final.pt", "metrics_raw": None, "model": tr.model_meta,
+                       "seed": args.seed, "world_size": info.world}, f)
+    if info.world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

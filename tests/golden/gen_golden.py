@@ -180,7 +180,7 @@ def gen_gae():
 
 
 def _sd_to_npz(sd):
-    return {"w::" + k: v.detach().cpu().numpy() for k, v in sd.items()}
+    return {"w::" + k: v.detach().cpu().numpy().copy() for k, v in sd.items()}
 
 
 def _sha(model):
@@ -258,7 +258,7 @@ def gen_ppo():
                                    mine_labels=labels, mine_valid=valid))
     cfg = PPOConfig(ent_coef=0.003, aux_mine_weight=0.05, aux_mine_calib_weight=0.01)
     stats = ppo_update(model, opt, batch, cfg, scaler=None)
-    post = {"post::" + k: v.detach().numpy() for k, v in model.state_dict().items()}
+    post = {"post::" + k: v.detach().numpy().copy() for k, v in model.state_dict().items()}
     np.savez_compressed(os.path.join(HERE, "ppo.npz"), obs=obs.numpy(), mask=mask.numpy(),
                         actions=actions.numpy(), old_logp=old_logp.numpy(), values=values.numpy(),
                         advantages=adv.numpy(), returns=rets.numpy(), mine_labels=labels.numpy(),

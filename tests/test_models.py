@@ -1,0 +1,83 @@
+"""Policy parity (CPU, fp32, eval mode) against outputs captured from the
+reference models (tests/golden/model_*.npz): logits/values/mine within 1e-5,
+and bit-identical seeded initialisation (state_dict sha256)."""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+
+
+def _sha(model):
+    h = hashlib.sha256()
+    for k, v in model.state_dict().items():
+        h.update(k.encode())
+        h.update(v.detach().cpu().contiguous().numpy().tobytes())
+    return h.hexdigest()
+
+
+@pytest.fixture(autouse=True)
+def _fp32():
+    prev = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision("highest")
+    yield
+    torch.set_float32_matmul_precision(prev)
+
+
+def test_small_model_outputs_from_golden_weights():
+    from ms_amd.models import build_model
+    z = golden("model_small.npz")
+    m = build_model("cnn_residual", obs_shape=(10, 16, 16),
+                    model_cfg=dict(stem_channels=16, blocks=2, dropout=0.05, value_hidden=32)).eval()
+    sd = {k[3:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("w::")}
+    missing, unexpected = m.load_state_dict(sd, strict=True), None
+    with torch.no_grad():
+        lg, v, mine = m(torch.from_numpy(z["obs"]), return_mine=True)
+    np.testing.assert_allclose(lg.numpy(), z["logits"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(v.numpy(), z["value"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(mine.numpy(), z["mine"], rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("H,W", [(16, 16), (9, 9), (30, 16)])
+def test_full_model_seeded_init_and_outputs(H, W):
+    from ms_amd.models import build_model
+    z = golden(f"model_full_{H}x{W}.npz")
+    torch.manual_seed(0)
+    m = build_model("cnn_residual", obs_shape=(10, H, W),
+                    model_cfg=dict(stem_channels=96, blocks=5, dropout=0.05, value_hidden=256)).eval()
+    assert sum(p.numel() for p in m.parameters()) == int(z["n_params"]) == 950947
+    assert _sha(m) == z["sha256"].item().decode()
+    with torch.no_grad():
+        lg, v, mine = m(torch.from_numpy(z["obs"]), return_mine=True)
+    np.testing.assert_allclose(lg.numpy(), z["logits"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(v.numpy(), z["value"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(mine.numpy(), z["mine"], rtol=0, atol=1e-5)
+
+
+def test_cnn_policy_seeded_init_and_outputs():
+    from ms_amd.models import build_model
+    z = golden("model_cnn_9x9.npz")
+    torch.manual_seed(0)
+    m = build_model("cnn", obs_shape=(10, 9, 9), model_cfg=dict(hidden=64)).eval()
+    assert _sha(m) == z["sha256"].item().decode()
+    with torch.no_grad():
+        lg, v, mine = m(torch.from_numpy(z["obs"]), return_mine=True)
+    np.testing.assert_allclose(lg.numpy(), z["logits"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(v.numpy(), z["value"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(mine.numpy(), z["mine"], rtol=0, atol=1e-5)
+
+
+def test_build_model_names_and_errors():
+    from ms_amd.models import CNNPolicy, CNNResidualPolicy, build_model, strip_compile_prefix
+    assert isinstance(build_model("cnn_large", obs_shape=(10, 8, 8)), CNNResidualPolicy)
+    assert isinstance(build_model("cnn", obs_shape=(10, 8, 8)), CNNPolicy)
+    with pytest.raises(ValueError):
+        build_model("transformer", obs_shape=(10, 8, 8))
+    with pytest.raises(ValueError):
+        CNNResidualPolicy(10, stem_channels=0)
+    sd = {"_orig_mod.stem.0.weight": 1, "_orig_mod.stem.0.bias": 2}
+    assert set(strip_compile_prefix(sd)) == {"stem.0.weight", "stem.0.bias"}

@@ -942,6 +942,7 @@ __global__ __launch_bounds__(256) void k_gae(const float* __restrict__ rewards, 
                                              const uint8_t* __restrict__ dones, const float* __restrict__ last_values,
                                              int T, int64_t N, float gamma, float gl, float* __restrict__ adv,
                                              float* __restrict__ ret) {
+#pragma clang fp contract(off)
   const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
   float last_adv = 0.f;
@@ -949,16 +950,18 @@ __global__ __launch_bounds__(256) void k_gae(const float* __restrict__ rewards, 
   for (int t = T - 1; t >= 0; --t) {
     const int64_t i = (int64_t)t * N + n;
     const float v = values[i];
-    const float nnt = __fsub_rn(1.0f, dones[i] ? 1.0f : 0.0f);
-    const float t1 = __fmul_rn(gamma, nv);
-    const float t2 = __fmul_rn(t1, nnt);
-    const float t3 = __fadd_rn(rewards[i], t2);
-    const float delta = __fsub_rn(t3, v);
-    const float t4 = __fmul_rn(gl, nnt);
-    const float t5 = __fmul_rn(t4, last_adv);
-    last_adv = __fadd_rn(delta, t5);
+    // plain operators under `fp contract(off)`: each op rounds to f32 (the
+    // __f*_rn helpers are header functions compiled with contraction on)
+    const float nnt = 1.0f - (dones[i] ? 1.0f : 0.0f);
+    const float t1 = gamma * nv;
+    const float t2 = t1 * nnt;
+    const float t3 = rewards[i] + t2;
+    const float delta = t3 - v;
+    const float t4 = gl * nnt;
+    const float t5 = t4 * last_adv;
+    last_adv = delta + t5;
     adv[i] = last_adv;
-    ret[i] = __fadd_rn(last_adv, v);
+    ret[i] = last_adv + v;
     nv = v;
   }
 }

@@ -1,0 +1,71 @@
+"""Micro-benchmark of one PPO minibatch update (fwd+bwd+AdamW) of the shipped
+model on synthetic 16x16 observations: where does the combined loop's time go?
+    python tools/ppo_micro.py --mb 32768 [--channels-last] [--benchmark] [--amp bf16]
+"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "minesweeper-ppo_amd"))
+import torch  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--mb", type=int, default=32768)
+ap.add_argument("--iters", type=int, default=6)
+ap.add_argument("--channels-last", action="store_true")
+ap.add_argument("--benchmark", action="store_true")
+ap.add_argument("--amp", default="bf16")
+ap.add_argument("--fwd-only", action="store_true")
+args = ap.parse_args()
+torch.backends.cudnn.benchmark = args.benchmark
+from ms_amd.models import build_model  # noqa: E402
+from ms_amd.ppo import PPOConfig, ppo_update  # noqa: E402
+from ms_amd.buffers import Batch  # noqa: E402
+
+dev = torch.device("cuda")
+torch.manual_seed(0)
+m = build_model("cnn_residual", obs_shape=(10, 16, 16),
+                model_cfg=dict(stem_channels=96, blocks=5, dropout=0.05, value_hidden=256)).to(dev)
+if args.channels_last:
+    m = m.to(memory_format=torch.channels_last)
+opt = torch.optim.AdamW(m.parameters(), lr=3e-4)
+M = args.mb
+g = torch.Generator(device=dev).manual_seed(0)
+rev = torch.rand(M, 16, 16, device=dev, generator=g) < 0.4
+cnt = torch.randint(0, 9, (M, 16, 16), device=dev, generator=g)
+obs = torch.zeros(M, 10, 16, 16, device=dev)
+obs[:, 0] = rev.float()
+obs.scatter_(1, (1 + cnt).unsqueeze(1), rev.float().unsqueeze(1))
+if args.channels_last:
+    obs = obs.contiguous(memory_format=torch.channels_last)
+mask = ~rev.view(M, -1)
+acts = torch.multinomial(mask.float() + 1e-6, 1, generator=g).squeeze(1)
+b = Batch(obs=obs, action_mask=mask, actions=acts, old_logp=-torch.rand(M, device=dev) * 5,
+          values=torch.randn(M, device=dev), advantages=torch.randn(M, device=dev),
+          returns=torch.randn(M, device=dev), mine_labels=(torch.rand(M, 16, 16, device=dev) < 0.15).float(),
+          mine_valid=~rev)
+cfg = PPOConfig(aux_mine_weight=0.05, aux_mine_calib_weight=0.01)
+amp = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": None}[args.amp]
+
+
+def step():
+    if args.fwd_only:
+        with torch.no_grad(), torch.autocast("cuda", dtype=amp, enabled=amp is not None):
+            m(obs)
+    else:
+        ppo_update(m, opt, b, cfg, amp_dtype=amp, sync_stats=False)
+
+
+for _ in range(2):
+    step()
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(args.iters):
+    step()
+torch.cuda.synchronize()
+dt = (time.perf_counter() - t0) / args.iters
+gf = (0.4388 if args.fwd_only else 1.3073) * M
+print(f"mb={M} cl={args.channels_last} bench={args.benchmark} amp={args.amp} fwd_only={args.fwd_only}: "
+      f"{dt * 1e3:.1f} ms/iter, {gf / dt / 1e3:.1f} TFLOP/s, mem {torch.cuda.max_memory_allocated() / 1e9:.1f} GB")

@@ -18,6 +18,7 @@ ap.add_argument("--channels-last", action="store_true")
 ap.add_argument("--benchmark", action="store_true")
 ap.add_argument("--amp", default="bf16")
 ap.add_argument("--fwd-only", action="store_true")
+ap.add_argument("--pure-bf16", action="store_true", help="model + obs in bf16, no autocast (timing only)")
 args = ap.parse_args()
 torch.backends.cudnn.benchmark = args.benchmark
 from ms_amd.models import build_model  # noqa: E402
@@ -28,6 +29,8 @@ dev = torch.device("cuda")
 torch.manual_seed(0)
 m = build_model("cnn_residual", obs_shape=(10, 16, 16),
                 model_cfg=dict(stem_channels=96, blocks=5, dropout=0.05, value_hidden=256)).to(dev)
+if args.pure_bf16:
+    m = m.to(torch.bfloat16)
 if args.channels_last:
     m = m.to(memory_format=torch.channels_last)
 opt = torch.optim.AdamW(m.parameters(), lr=3e-4)
@@ -38,6 +41,8 @@ cnt = torch.randint(0, 9, (M, 16, 16), device=dev, generator=g)
 obs = torch.zeros(M, 10, 16, 16, device=dev)
 obs[:, 0] = rev.float()
 obs.scatter_(1, (1 + cnt).unsqueeze(1), rev.float().unsqueeze(1))
+if args.pure_bf16:
+    obs = obs.to(torch.bfloat16)
 if args.channels_last:
     obs = obs.contiguous(memory_format=torch.channels_last)
 mask = ~rev.view(M, -1)
@@ -48,6 +53,9 @@ b = Batch(obs=obs, action_mask=mask, actions=acts, old_logp=-torch.rand(M, devic
           mine_valid=~rev)
 cfg = PPOConfig(aux_mine_weight=0.05, aux_mine_calib_weight=0.01)
 amp = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": None}[args.amp]
+if args.pure_bf16:
+    amp = None
+    b.mine_labels = b.mine_labels.bfloat16()
 
 
 def step():

@@ -35,6 +35,19 @@ def algo_bytes_per_env_step(H: int, W: int) -> int:
     return 40 * A + A + 8 + 4 + 1 + 12 + 2 * (2 * ((A + 7) // 8) + 32) + 16
 
 
+def pmc_traffic(H, W, K, n):
+    """HBM bytes per k_step launch from the committed rocprofv3 PMC passes
+    (FETCH_SIZE + WRITE_SIZE, separate passes; tools/profile_round.sh) of the
+    latest round under profiles/, for this exact board and env count."""
+    import glob
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_k_step_{H}x{W}x{K}_{n}.json")))
+    if not cands:
+        return None, None
+    with open(cands[-1]) as f:
+        d = json.load(f)
+    return d["traffic_bytes_per_launch"], os.path.relpath(cands[-1], ROOT)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -214,19 +227,31 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
-    # Dominant-kernel duration: HIP events around each ms_step on its stream,
-    # over a pass of the same K steps right after the timed region.
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
+    # Dominant-kernel duration: HIP events around each ms_step on its stream, over
+    # a pass of the same K steps right after the timed region; the cost of an
+    # empty event pair at the same stream position (after a tape kernel) is
+    # measured and subtracted (the raw figure is reported too).
+    def ev_pair():
+        return torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    events = [ev_pair() for _ in range(args.steps)]
+    empties = [ev_pair() for _ in range(args.steps)]
+    base_t = args.warmup + args.steps
     for k in range(args.steps):
-        one_step(args.warmup + args.steps + k, sp, events[k])
+        one_step(base_t + k, sp, events[k])
+    for k in range(args.steps):  # same shape: tape kernel, then an empty event pair
+        L.check(lib.ms_tape_actions(h, base_t + args.steps + k, args.tape, ptrs[0], sp))
+        empties[k][0].record()
+        empties[k][1].record()
     torch.cuda.synchronize()
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    kern_raw_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    ev_overhead_ms = float(np.mean([a.elapsed_time(b) for a, b in empties]))
+    kern_ms = max(kern_raw_ms - ev_overhead_ms, 1e-6)
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kern_ms, kern_raw_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+        elapsed, kern_ms, kern_raw_ms = float(t[0]), float(t[1]), float(t[2])
 
+    traffic, traffic_src = pmc_traffic(H, W, K, n_local)
     total_env_steps = n_total * args.steps
     value = total_env_steps / elapsed
     bpe = algo_bytes_per_env_step(H, W)
@@ -250,8 +275,10 @@ def main():
                    "board": f"{H}x{W}x{K}", "envs_per_gpu": n_local, "envs_total": n_total,
                    "tape": args.tape, "parallelism": f"env-shard x{world}, no collective"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "k_step", "kernel_ms": kern_ms, "algo_bytes_per_env_step": bpe},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "k_step", "kernel_ms": kern_ms, "kernel_ms_raw_events": kern_raw_ms,
+                     "event_pair_overhead_ms": ev_overhead_ms, "algo_bytes_per_env_step": bpe,
+                     "algo_bytes_per_launch": bpe * n_local, "traffic_source": traffic_src},
     }
     if args.ppo_updates > 0:
         out["ppo"] = ppo_bench(args, world, rank, local_rank, dev)

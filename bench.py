@@ -204,52 +204,63 @@ def main():
 
     # Timed region: the K steps (2K kernel launches) are captured once into a
     # HIP graph and replayed, so host launch cost is off the critical path.
-    graph = None
-    if args.graph:
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+    def capture(tape_only: bool):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
             cs = torch.cuda.current_stream().cuda_stream
             for k in range(args.steps):
-                one_step(args.warmup + k, cs)
+                if tape_only:
+                    L.check(lib.ms_tape_actions(h, args.warmup + k, args.tape, ptrs[0], cs))
+                else:
+                    one_step(args.warmup + k, cs)
         torch.cuda.synchronize()
-        # capture does not execute: the board state is still at step `warmup`
+        return g  # capture does not execute: the board state is still at step `warmup`
+
+    graph = capture(False) if args.graph else None
+    ev_full = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev_full[0].record()
     if graph is not None:
         graph.replay()
     else:
         for k in range(args.steps):
             one_step(args.warmup + k, sp)
+    ev_full[1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
-    # Dominant-kernel duration: HIP events around each ms_step on its stream, over
-    # a pass of the same K steps right after the timed region; the cost of an
-    # empty event pair at the same stream position (after a tape kernel) is
-    # measured and subtracted (the raw figure is reported too).
-    def ev_pair():
-        return torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    events = [ev_pair() for _ in range(args.steps)]
-    empties = [ev_pair() for _ in range(args.steps)]
-    base_t = args.warmup + args.steps
-    for k in range(args.steps):
-        one_step(base_t + k, sp, events[k])
-    for k in range(args.steps):  # same shape: tape kernel, then an empty event pair
-        L.check(lib.ms_tape_actions(h, base_t + args.steps + k, args.tape, ptrs[0], sp))
-        empties[k][0].record()
-        empties[k][1].record()
-    torch.cuda.synchronize()
-    kern_raw_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
-    ev_overhead_ms = float(np.mean([a.elapsed_time(b) for a, b in empties]))
-    kern_ms = max(kern_raw_ms - ev_overhead_ms, 1e-6)
+    # Dominant-kernel duration from HIP events on the launch stream: the span of
+    # the K-step graph minus the span of a graph holding only its K tape
+    # launches, divided by K = what one ms_step adds to a step, boundary
+    # included (rocprofv3's per-dispatch average is in profiles/).
+    if graph is not None:
+        gt = capture(True)
+        ev_tape = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev_tape[0].record()
+        gt.replay()
+        ev_tape[1].record()
+        torch.cuda.synchronize()
+        span_full = ev_full[0].elapsed_time(ev_full[1])
+        span_tape = ev_tape[0].elapsed_time(ev_tape[1])
+        kern_ms = (span_full - span_tape) / args.steps
+        kern_method = "graph span difference (tape+step vs tape only) / K"
+    else:
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        for k in range(args.steps):
+            one_step(args.warmup + args.steps + k, sp, evs[k])
+        torch.cuda.synchronize()
+        kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        kern_method = "events around each ms_step (eager)"
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms, kern_raw_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms, kern_raw_ms = float(t[0]), float(t[1]), float(t[2])
+        elapsed, kern_ms = float(t[0]), float(t[1])
 
     traffic, traffic_src = pmc_traffic(H, W, K, n_local)
     total_env_steps = n_total * args.steps
@@ -276,8 +287,8 @@ def main():
                    "tape": args.tape, "parallelism": f"env-shard x{world}, no collective"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_step", "kernel_ms": kern_ms, "kernel_ms_raw_events": kern_raw_ms,
-                     "event_pair_overhead_ms": ev_overhead_ms, "algo_bytes_per_env_step": bpe,
+                     "kernel": "k_step", "kernel_ms": kern_ms, "kernel_ms_method": kern_method,
+                     "algo_bytes_per_env_step": bpe,
                      "algo_bytes_per_launch": bpe * n_local, "traffic_source": traffic_src},
     }
     if args.ppo_updates > 0:

@@ -882,49 +882,59 @@ __device__ __forceinline__ int select_bit(uint64_t x, uint32_t k) {  // k-th set
 }
 
 
-// Lane-per-env form: each thread reads its env's packed row words (one
-// coalesced 32 B run per env on 16x16), counts and selects in registers. Bit b
-// of word w is cell w*RPW*W + b (rows are packed back to back inside a word).
-__global__ __launch_bounds__(64) void k_tape(const uint64_t* __restrict__ mw, const uint64_t* __restrict__ rw,
-                                             int64_t n, int H, int W, int64_t env_begin, uint64_t t, int mode,
-                                             int64_t* __restrict__ actions) {
-  const int64_t env = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// exclusive prefix sum over the wave: Kogge-Stone inside 16-lane rows
+// (row_shr 1/2/4/8), then row_bcast15 / row_bcast31 carry across rows (GFX9 DPP)
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v) {
+  uint32_t s = v;
+  s += dpp32<0x111>(s);
+  s += dpp32<0x112>(s);
+  s += dpp32<0x114>(s);
+  s += dpp32<0x118>(s);
+  s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x142, 0xa, 0xf, false);
+  s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x143, 0xc, 0xf, false);
+  return s - v;
+}
+
+__global__ __launch_bounds__(64) void k_tape(const uint64_t* mw, const uint64_t* rw, int64_t n, int H, int W,
+                                             int64_t env_begin, uint64_t t, int mode, int64_t* actions) {
+  const int lane = lane_id();
+  const int64_t env = blockIdx.x;
   if (env >= n) return;
-  const int rpw = 64 / W, NW = (H + rpw - 1) / rpw, span = rpw * W;
-  const uint64_t full = span == 64 ? ~0ull : ((1ull << span) - 1ull);
-  const uint64_t* m = mw + env * NW;
-  const uint64_t* r = rw + env * NW;
+  const Geo<0, 0> g(H, W);
+  const int NW = g.NW();
+  const uint64_t mine = load_row(mw + env * NW, g, lane);
+  const uint64_t rev = load_row(rw + env * NW, g, lane);
+  const uint64_t valid = ~rev & g.rowmask() & (lane < H ? ~0ull : 0ull);
+  const uint64_t safe = valid & ~mine;
   const uint64_t gidx = (uint64_t)(env_begin + env);
   const uint64_t x = splitmix64(0xC0FFEEull ^ (gidx << 32) ^ t);
-  const bool safe_mode = mode == MS_TAPE_SAFE_BIASED;
-  uint32_t n_valid = 0, n_safe = 0;
-  for (int w = 0; w < NW; ++w) {
-    const int rows = min(rpw, H - w * rpw);
-    const uint64_t lim = rows * W == 64 ? ~0ull : ((1ull << (rows * W)) - 1ull);
-    const uint64_t v = ~r[w] & full & lim;
-    n_valid += (uint32_t)__popcll(v);
-    if (safe_mode) n_safe += (uint32_t)__popcll(v & ~m[w]);
+  const uint32_t n_valid = wave_sum((uint32_t)__popcll(valid));
+  const uint32_t n_safe = wave_sum((uint32_t)__popcll(safe));
+  const bool want_safe = mode == MS_TAPE_SAFE_BIASED && (x & 0xFFFFull) < 65208ull && n_safe > 0;
+  uint64_t bits;
+  uint32_t cnt;
+  uint64_t sel;
+  if (want_safe) {
+    bits = safe;
+    cnt = n_safe;
+    sel = x >> 16;
+  } else {
+    bits = valid;
+    cnt = n_valid;
+    sel = (mode == MS_TAPE_SAFE_BIASED) ? (x >> 16) : x;
   }
-  const bool want_safe = safe_mode && (x & 0xFFFFull) < 65208ull && n_safe > 0;
-  const uint32_t cnt = want_safe ? n_safe : n_valid;
-  const uint64_t sel = safe_mode ? (x >> 16) : x;
   int64_t act = 0;
   if (cnt > 0) {
-    uint32_t target = (uint32_t)(sel % (uint64_t)cnt);
-    for (int w = 0; w < NW; ++w) {
-      const int rows = min(rpw, H - w * rpw);
-      const uint64_t lim = rows * W == 64 ? ~0ull : ((1ull << (rows * W)) - 1ull);
-      uint64_t v = ~r[w] & full & lim;
-      if (want_safe) v &= ~m[w];
-      const uint32_t pc = (uint32_t)__popcll(v);
-      if (target < pc) {
-        act = (int64_t)w * span + select_bit(v, target);
-        break;
-      }
-      target -= pc;
-    }
+    const uint32_t target = (uint32_t)(sel % (uint64_t)cnt);
+    const uint32_t pc = (uint32_t)__popcll(bits);
+    const uint32_t before = wave_excl_scan(pc);
+    const bool mine_lane = target >= before && target < before + pc;
+    const uint64_t who = __ballot(mine_lane);
+    const int src = __ffsll((unsigned long long)who) - 1;
+    const int col = (int)readlane32((uint32_t)(mine_lane ? select_bit(bits, target - before) : 0), src);
+    act = (int64_t)src * W + col;
   }
-  actions[env] = act;
+  if (lane == 0) actions[env] = act;
 }
 
 // ---------------------------------------------------------------------------
@@ -1337,7 +1347,7 @@ int ms_rng_state(ms_handle* h, uint64_t* out, void* stream) {
 int ms_tape_actions(ms_handle* h, uint64_t t, int32_t mode, int64_t* actions, void* stream) {
   if (!h || !actions) return fail(MS_EINVAL, "ms_tape_actions: null argument");
   if (mode != MS_TAPE_UNIFORM && mode != MS_TAPE_SAFE_BIASED) return fail(MS_EINVAL, "ms_tape_actions: bad mode");
-  hipLaunchKernelGGL(k_tape, dim3((unsigned)((h->n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, h->mine_words,
+  hipLaunchKernelGGL(k_tape, dim3((unsigned)h->n), dim3(64), 0, (hipStream_t)stream, h->mine_words,
                      h->rev_words, h->n, h->H, h->W, h->env_begin, t, mode, actions);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? MS_OK : hip_fail(e, "ms_tape_actions launch");

@@ -1,0 +1,38 @@
+/*
+ * mscnn.h — C ABI of the fused residual-CNN kernels (libmsenv.so).
+ *
+ * Replaces, for the shipped CNNResidualPolicy (minesweeper/models/cnn_residual.py:7-96),
+ * the PyTorch op chain conv3x3 -> GroupNorm(C/16 groups) -> [+residual] -> ReLU
+ * -> [Dropout2d] of one stem / half-block (cnn_residual.py:10-26, 50-54) with
+ * one MFMA implicit-GEMM kernel per sample-workgroup, and its backward.
+ *
+ * Layouts: activations NHWC bf16 [N][H*W][C]; conv weights bf16 [9][COUT][CIN]
+ * (tap-major, tap = 3*(dy+1) + (dx+1)); per-channel params f32. COUT = 96.
+ * All pointers are device pointers; `stream` is a hipStream_t (void*).
+ * Returns 0 on success, MS_EINVAL / MS_EHIP (msenv.h) otherwise.
+ */
+#ifndef MSCNN_H
+#define MSCNN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Forward of one fused layer:
+ *   y   = conv3x3(x, w) + bias                       (saved to ysave, bf16)
+ *   out = relu(GN(y) * gamma + beta [+ res]) [* dmask[n][c]]
+ * cin in {16, 96} (the stem's 10 input planes are zero-padded to 16).
+ * res (bf16 [N][P][96]), dmask (f32 [N][96], 0 or 1/(1-p)), ysave and stats
+ * (f32 [N][6][2] = mean, rstd per group) may be NULL. */
+int mc_conv_gn_fwd(const uint16_t* x, const uint16_t* w, const float* bias, const float* gamma,
+                   const float* beta, const uint16_t* res, const float* dmask, uint16_t* out,
+                   uint16_t* ysave, float* stats, int32_t n, int32_t h, int32_t w_, int32_t cin,
+                   float eps, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MSCNN_H */

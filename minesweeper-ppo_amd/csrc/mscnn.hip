@@ -1,0 +1,310 @@
+// mscnn.hip — fused conv3x3 + GroupNorm + residual + ReLU + dropout (gfx950 MFMA).
+//
+// Reference op chain (minesweeper/models/cnn_residual.py:10-26, 50-54):
+//   y = Conv2d(C, 96, 3, padding=1)(x); y = GroupNorm(6, 96)(y); [y += residual]; y = ReLU(y);
+//   [y = Dropout2d(p)(y)]
+// PyTorch runs this as ~8 kernels per layer (MIOpen conv with NCHW<->NHWC
+// transposes, bf16<->f32 casts, 4 GroupNorm kernels, elementwise), 70 % of the
+// PPO-update time being glue (profiles/r01/ppo_minibatch_kernel_stats.csv).
+//
+// Here: one persistent workgroup (4 waves) per sample at a time. The sample's
+// NHWC bf16 input tile (with a zero halo) sits in LDS; the conv is an implicit
+// GEMM out[px][co] = sum_{tap,ci} x[px+tap][ci] * w[tap][co][ci] on
+// v_mfma_f32_32x32x16_bf16 (A = 32 pixels x 16 ci read straight from the halo
+// tile, B = 16 ci x 32 co from the tap's LDS-staged weights). Each wave owns
+// NPT 32-pixel tiles x all 96 output channels, so a whole GroupNorm group
+// (16 channels x all pixels of the sample) lives in the workgroup: mean and
+// variance (two-pass) are reduced with DPP row sums + an LDS exchange across
+// the 4 waves, and normalisation, affine, residual, ReLU and the dropout scale
+// are applied in the epilogue before a single bf16 store.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../../include/msenv.h"
+#include "../../include/mscnn.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int COUT = 96;
+constexpr int NGRP = 6;  // GroupNorm groups (96 / 16)
+constexpr int WAVES = 4;
+
+thread_local char g_err[256] = "";
+
+struct FwdParams {
+  const __bf16* x;
+  const __bf16* wt;
+  const float* bias;
+  const float* gamma;
+  const float* beta;
+  const __bf16* res;
+  const float* dmask;
+  __bf16* out;
+  __bf16* ysave;
+  float* stats;
+  int N, H, W;
+  float eps;
+};
+
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, true));
+}
+
+// sum over each 16-lane row; the result is valid in lanes 15, 31, 47, 63
+__device__ __forceinline__ float row_sum16(float v) {
+  v += dppf<0x111>(v);
+  v += dppf<0x112>(v);
+  v += dppf<0x114>(v);
+  v += dppf<0x118>(v);
+  return v;
+}
+
+__device__ __forceinline__ float readlane_f(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+
+// LDS layout (bf16 elements): sX[(H+2)*(W+2)][CINP] halo tile, sW[COUT][CINP]
+// one tap of weights; then f32 sRed[WAVES][NGRP].
+template <int CIN>
+constexpr int cinp() { return CIN + 8; }  // +16 B per pixel row: conflict-free ds_read_b128
+
+template <int CIN, int NPT>
+__global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int CINP = cinp<CIN>();
+  const int H = p.H, W = p.W, P = H * W, WP = W + 2;
+  __bf16* sX = reinterpret_cast<__bf16*>(smem);
+  __bf16* sW = sX + (H + 2) * WP * CINP;
+  float* sRed = reinterpret_cast<float*>(sW + COUT * CINP);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+
+  // zero the halo tile once: the border is never overwritten
+  {
+    uint4* z = reinterpret_cast<uint4*>(sX);
+    const int nz = (H + 2) * WP * CINP / 8;
+    for (int i = tid; i < nz; i += 256) z[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  int aoff[NPT];
+  bool aval[NPT];
+#pragma unroll
+  for (int t = 0; t < NPT; ++t) {
+    const int px = (wave * NPT + t) * 32 + l32;
+    aval[t] = px < P;
+    const int r = aval[t] ? px / W : 0, c = aval[t] ? px - r * W : 0;
+    aoff[t] = ((r + 1) * WP + (c + 1)) * CINP + 8 * hh;
+  }
+
+  for (int n = blockIdx.x; n < p.N; n += gridDim.x) {
+    __syncthreads();  // previous sample's epilogue is done with sX/sRed
+    {  // input tile -> LDS interior
+      const uint4* xs = reinterpret_cast<const uint4*>(p.x + (size_t)n * P * CIN);
+      constexpr int C8 = CIN / 8;
+      for (int i = tid; i < P * C8; i += 256) {
+        const int px = i / C8, c8 = i - px * C8;
+        const int r = px / W, c = px - r * W;
+        *reinterpret_cast<uint4*>(&sX[((r + 1) * WP + c + 1) * CINP + c8 * 8]) = xs[i];
+      }
+    }
+    f32x16 acc[NPT][3];
+#pragma unroll
+    for (int t = 0; t < NPT; ++t)
+#pragma unroll
+      for (int ct = 0; ct < 3; ++ct)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[t][ct][i] = 0.f;
+
+    for (int tap = 0; tap < 9; ++tap) {
+      __syncthreads();  // sW free (previous tap done); sX writes visible
+      {
+        const uint4* ws = reinterpret_cast<const uint4*>(p.wt + (size_t)tap * COUT * CIN);
+        constexpr int C8 = CIN / 8;
+        for (int i = tid; i < COUT * C8; i += 256) {
+          const int co = i / C8, c8 = i - co * C8;
+          *reinterpret_cast<uint4*>(&sW[co * CINP + c8 * 8]) = ws[i];
+        }
+      }
+      __syncthreads();
+      const int dr = tap / 3 - 1, dc = tap % 3 - 1;
+      const int tshift = (dr * WP + dc) * CINP;
+#pragma unroll
+      for (int k0 = 0; k0 < CIN; k0 += 16) {
+        bf16x8 b[3];
+#pragma unroll
+        for (int ct = 0; ct < 3; ++ct)
+          b[ct] = *reinterpret_cast<const bf16x8*>(&sW[(ct * 32 + l32) * CINP + k0 + 8 * hh]);
+#pragma unroll
+        for (int t = 0; t < NPT; ++t) {
+          bf16x8 a = *reinterpret_cast<const bf16x8*>(&sX[aoff[t] + tshift + k0]);
+          if (!aval[t]) a = bf16x8{};
+#pragma unroll
+          for (int ct = 0; ct < 3; ++ct) acc[t][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[ct], acc[t][ct], 0, 0, 0);
+        }
+      }
+    }
+
+    // ---------------- epilogue: bias, GroupNorm, residual, ReLU, dropout ----------------
+    float biasv[3];
+#pragma unroll
+    for (int ct = 0; ct < 3; ++ct) biasv[ct] = p.bias[ct * 32 + l32];
+    float mean[3], rstd[3];  // this lane's group statistics, per co tile
+    const float inv_cnt = 1.0f / (16.0f * (float)P);
+    for (int pass = 0; pass < 2; ++pass) {
+      float part[3];
+#pragma unroll
+      for (int ct = 0; ct < 3; ++ct) {
+        float s = 0.f;
+#pragma unroll
+        for (int t = 0; t < NPT; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int px = (wave * NPT + t) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+            if (px < P) {
+              const float v = acc[t][ct][i] + biasv[ct];
+              s += pass == 0 ? v : (v - mean[ct]) * (v - mean[ct]);
+            }
+          }
+        part[ct] = row_sum16(s);
+      }
+      __syncthreads();  // sRed reuse across passes
+      if (lane == 0) {
+#pragma unroll
+        for (int ct = 0; ct < 3; ++ct) {
+          // rows 0/2 (lanes 0-15, 32-47) hold channels ct*32+0..15 = group 2ct,
+          // rows 1/3 hold group 2ct+1
+          sRed[wave * NGRP + 2 * ct] = readlane_f(part[ct], 15) + readlane_f(part[ct], 47);
+          sRed[wave * NGRP + 2 * ct + 1] = readlane_f(part[ct], 31) + readlane_f(part[ct], 63);
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int ct = 0; ct < 3; ++ct) {
+        const int g = 2 * ct + (l32 >> 4);
+        float tot = 0.f;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) tot += sRed[w * NGRP + g];
+        if (pass == 0) {
+          mean[ct] = tot * inv_cnt;
+        } else {
+          rstd[ct] = rsqrtf(tot * inv_cnt + p.eps);
+        }
+      }
+    }
+    if (p.stats && wave == 0 && (l32 & 15) == 0 && hh == 0) {
+#pragma unroll
+      for (int ct = 0; ct < 3; ++ct) {
+        const int g = 2 * ct + (l32 >> 4);
+        p.stats[((size_t)n * NGRP + g) * 2 + 0] = mean[ct];
+        p.stats[((size_t)n * NGRP + g) * 2 + 1] = rstd[ct];
+      }
+    }
+#pragma unroll
+    for (int ct = 0; ct < 3; ++ct) {
+      const int co = ct * 32 + l32;
+      const float ga = p.gamma[co] * rstd[ct];
+      const float be = p.beta[co] - mean[ct] * ga;
+      const float dm = p.dmask ? p.dmask[(size_t)n * COUT + co] : 1.0f;
+#pragma unroll
+      for (int t = 0; t < NPT; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int px = (wave * NPT + t) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          if (px < P) {
+            const size_t o = ((size_t)n * P + px) * COUT + co;
+            const float v = acc[t][ct][i] + biasv[ct];
+            float z = v * ga + be;
+            if (p.res) z += (float)p.res[o];
+            z = fmaxf(z, 0.f) * dm;
+            p.out[o] = (__bf16)z;
+            if (p.ysave) p.ysave[o] = (__bf16)v;
+          }
+        }
+    }
+  }
+}
+
+template <int CIN, int NPT>
+int launch_fwd(const FwdParams& p, hipStream_t s) {
+  constexpr int CINP = cinp<CIN>();
+  const size_t lds = (size_t)(p.H + 2) * (p.W + 2) * CINP * 2 + (size_t)COUT * CINP * 2 + WAVES * NGRP * 4;
+  if (lds > 160 * 1024) {
+    snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd: board %dx%d needs %zu B LDS", p.H, p.W, lds);
+    return MS_EINVAL;
+  }
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)k_conv_gn_fwd<CIN, NPT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr_set = true;
+  }
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const int grid = p.N < ncu ? p.N : ncu;
+  hipLaunchKernelGGL((k_conv_gn_fwd<CIN, NPT>), dim3(grid), dim3(256), lds, s, p);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd launch: %s", hipGetErrorString(e));
+    return MS_EHIP;
+  }
+  return MS_OK;
+}
+
+template <int CIN>
+int dispatch_fwd(const FwdParams& p, hipStream_t s) {
+  const int P = p.H * p.W;
+  const int tiles = (P + 31) / 32;
+  const int npt = (tiles + WAVES - 1) / WAVES;
+  switch (npt) {
+    case 1: return launch_fwd<CIN, 1>(p, s);
+    case 2: return launch_fwd<CIN, 2>(p, s);
+    case 3: return launch_fwd<CIN, 3>(p, s);
+    case 4: return launch_fwd<CIN, 4>(p, s);
+    default:
+      snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd: %d pixels > 512 unsupported", P);
+      return MS_EINVAL;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* mc_last_error(void) { return g_err; }
+
+int mc_conv_gn_fwd(const uint16_t* x, const uint16_t* w, const float* bias, const float* gamma, const float* beta,
+                   const uint16_t* res, const float* dmask, uint16_t* out, uint16_t* ysave, float* stats, int32_t n,
+                   int32_t h, int32_t w_, int32_t cin, float eps, void* stream) {
+  if (!x || !w || !bias || !gamma || !beta || !out || n <= 0 || h <= 0 || w_ <= 0) {
+    snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd: bad argument");
+    return MS_EINVAL;
+  }
+  FwdParams p;
+  p.x = reinterpret_cast<const __bf16*>(x);
+  p.wt = reinterpret_cast<const __bf16*>(w);
+  p.bias = bias;
+  p.gamma = gamma;
+  p.beta = beta;
+  p.res = reinterpret_cast<const __bf16*>(res);
+  p.dmask = dmask;
+  p.out = reinterpret_cast<__bf16*>(out);
+  p.ysave = reinterpret_cast<__bf16*>(ysave);
+  p.stats = stats;
+  p.N = n;
+  p.H = h;
+  p.W = w_;
+  p.eps = eps;
+  hipStream_t s = (hipStream_t)stream;
+  if (cin == 16) return dispatch_fwd<16>(p, s);
+  if (cin == 96) return dispatch_fwd<96>(p, s);
+  snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd: cin %d unsupported (16 or 96)", cin);
+  return MS_EINVAL;
+}
+
+}  // extern "C"

@@ -1,0 +1,82 @@
+"""Fused MFMA residual-CNN layer ops (csrc/mscnn.hip, C ABI include/mscnn.h).
+
+Activations are NHWC bf16 [N, H*W, C]; weights are re-laid out per call as
+bf16 [9, 96, CIN] (tap-major). These ops replace, for CNNResidualPolicy
+(minesweeper/models/cnn_residual.py:7-96), the chain conv3x3 -> GroupNorm ->
+[+residual] -> ReLU -> [Dropout2d] with one kernel per layer.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib as L
+
+COUT = 96
+NGROUPS = 6
+
+
+def _fn(name, argtypes):
+    lib = L.load()
+    f = getattr(lib, name)
+    f.argtypes = argtypes
+    f.restype = ctypes.c_int
+    return f
+
+
+_vp, _i32, _f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_float
+_fwd = None
+
+
+def _check(rc):
+    if rc != 0:
+        lib = L.load()
+        lib.mc_last_error.restype = ctypes.c_char_p
+        raise L.MsEnvError(lib.mc_last_error().decode(errors="replace"))
+
+
+def prep_weight(w: torch.Tensor, cin_pad: int) -> torch.Tensor:
+    """[96, cin, 3, 3] (f32 nn.Conv2d weight) -> bf16 [9, 96, cin_pad], tap = 3*ky + kx."""
+    co, ci = w.shape[0], w.shape[1]
+    wt = w.permute(2, 3, 0, 1).reshape(9, co, ci)
+    if cin_pad > ci:
+        wt = torch.nn.functional.pad(wt, (0, cin_pad - ci))
+    return wt.to(torch.bfloat16).contiguous()
+
+
+def obs_to_nhwc(obs: torch.Tensor, cin_pad: int = 16) -> torch.Tensor:
+    """f32 [N, 10, H, W] one-hot observation -> bf16 [N, H*W, cin_pad] (exact: values are 0/1)."""
+    n, c, h, w = obs.shape
+    x = obs.permute(0, 2, 3, 1).reshape(n, h * w, c)
+    if cin_pad > c:
+        x = torch.nn.functional.pad(x, (0, cin_pad - c))
+    return x.to(torch.bfloat16).contiguous()
+
+
+def conv_gn_fwd(x: torch.Tensor, wt: torch.Tensor, bias: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor,
+                H: int, W: int, res: Optional[torch.Tensor] = None, dmask: Optional[torch.Tensor] = None,
+                save: bool = True, eps: float = 1e-5
+                ) -> Tuple[torch.Tensor, Optional[torch.Tensor], Optional[torch.Tensor]]:
+    """out = relu(GN(conv3x3(x) + bias) * gamma + beta [+ res]) [* dmask]; returns (out, y, stats)."""
+    global _fwd
+    if _fwd is None:
+        _fwd = _fn("mc_conv_gn_fwd", [_vp] * 10 + [_i32] * 4 + [_f32, _vp])
+    n, p, cin = x.shape
+    assert p == H * W and x.dtype == torch.bfloat16 and x.is_contiguous()
+    assert wt.shape == (9, COUT, cin) and wt.dtype == torch.bfloat16 and wt.is_contiguous()
+    dev = x.device
+    out = torch.empty((n, p, COUT), dtype=torch.bfloat16, device=dev)
+    y = torch.empty_like(out) if save else None
+    stats = torch.empty((n, NGROUPS, 2), dtype=torch.float32, device=dev) if save else None
+    if res is not None:
+        assert res.shape == out.shape and res.dtype == torch.bfloat16 and res.is_contiguous()
+    if dmask is not None:
+        dmask = dmask.to(torch.float32).contiguous()
+        assert dmask.shape == (n, COUT)
+    f32c = lambda t: t.detach().to(torch.float32).contiguous()  # noqa: E731
+    b, g, be = f32c(bias), f32c(gamma), f32c(beta)
+    _check(_fwd(L.ptr(x), L.ptr(wt), L.ptr(b), L.ptr(g), L.ptr(be), L.ptr(res), L.ptr(dmask), L.ptr(out),
+                L.ptr(y), L.ptr(stats), n, H, W, cin, eps, L.stream_ptr(dev)))
+    return out, y, stats

@@ -172,14 +172,22 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
           }
         part[ct] = row_sum16(s);
       }
+      // rows 0/2 (lanes 0-15, 32-47) hold channels ct*32+0..15 = group 2ct, rows
+      // 1/3 group 2ct+1. The readlanes stay in converged control flow: inside a
+      // lane-0 branch the compiler may sink the last DPP add into the branch and
+      // the readlane would see the other lanes' stale values.
+      float gs[3][2];
+#pragma unroll
+      for (int ct = 0; ct < 3; ++ct) {
+        gs[ct][0] = readlane_f(part[ct], 15) + readlane_f(part[ct], 47);
+        gs[ct][1] = readlane_f(part[ct], 31) + readlane_f(part[ct], 63);
+      }
       __syncthreads();  // sRed reuse across passes
       if (lane == 0) {
 #pragma unroll
         for (int ct = 0; ct < 3; ++ct) {
-          // rows 0/2 (lanes 0-15, 32-47) hold channels ct*32+0..15 = group 2ct,
-          // rows 1/3 hold group 2ct+1
-          sRed[wave * NGRP + 2 * ct] = readlane_f(part[ct], 15) + readlane_f(part[ct], 47);
-          sRed[wave * NGRP + 2 * ct + 1] = readlane_f(part[ct], 31) + readlane_f(part[ct], 63);
+          sRed[wave * NGRP + 2 * ct] = gs[ct][0];
+          sRed[wave * NGRP + 2 * ct + 1] = gs[ct][1];
         }
       }
       __syncthreads();

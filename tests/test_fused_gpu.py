@@ -22,8 +22,9 @@ def _ref(x, w, b, g, be, H, W, res=None, dmask=None):
     if dmask is not None:
         z = z * dmask[:, :, None, None]
     to_nhwc = lambda t: t.permute(0, 2, 3, 1).reshape(n, p, 96)  # noqa: E731
-    mean = y.view(n, 6, -1).mean(-1)
-    rstd = torch.rsqrt(y.view(n, 6, -1).var(-1, unbiased=False) + 1e-5)
+    y = y.contiguous()
+    mean = y.reshape(n, 6, -1).mean(-1)
+    rstd = torch.rsqrt(y.reshape(n, 6, -1).var(-1, unbiased=False) + 1e-5)
     return to_nhwc(z), to_nhwc(y), torch.stack([mean, rstd], -1)
 
 

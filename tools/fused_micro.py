@@ -1,0 +1,55 @@
+"""Time the fused conv+GN+ReLU MFMA kernel against the PyTorch (MIOpen) chain
+for one layer at the PPO minibatch size. python tools/fused_micro.py [--n 32768]"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "minesweeper-ppo_amd"))
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+from ms_amd.fused import conv_gn_fwd, prep_weight  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=32768)
+ap.add_argument("--hw", default="16x16")
+ap.add_argument("--iters", type=int, default=10)
+args = ap.parse_args()
+H, W = (int(v) for v in args.hw.split("x"))
+dev = torch.device("cuda")
+n, P = args.n, H * W
+x = (torch.randn(n, P, 96, device=dev) * 0.5).to(torch.bfloat16)
+w = torch.randn(96, 96, 3, 3, device=dev) * 0.03
+b, g, be = torch.zeros(96, device=dev), torch.ones(96, device=dev), torch.zeros(96, device=dev)
+wt = prep_weight(w, 96)
+res = torch.randn(n, P, 96, device=dev).to(torch.bfloat16)
+
+
+def t(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters
+
+
+flop = 2 * n * P * 96 * 864
+f1 = t(lambda: conv_gn_fwd(x, wt, b, g, be, H, W, res=res), args.iters)
+print(f"fused conv+GN+res+ReLU  n={n} {H}x{W}: {f1 * 1e3:.2f} ms  {flop / f1 / 1e12:.0f} TFLOP/s(conv)", flush=True)
+xn = x.float().view(n, H, W, 96).permute(0, 3, 1, 2).contiguous().to(torch.bfloat16)
+rn = res.float().view(n, H, W, 96).permute(0, 3, 1, 2).contiguous().to(torch.bfloat16)
+conv = torch.nn.Conv2d(96, 96, 3, padding=1).to(dev)
+gn = torch.nn.GroupNorm(6, 96).to(dev)
+
+
+def torch_chain():
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        return torch.relu(gn(conv(xn)) + rn)
+
+
+f2 = t(torch_chain, args.iters)
+print(f"torch conv+GN+res+ReLU (bf16 autocast, NCHW): {f2 * 1e3:.2f} ms  {flop / f2 / 1e12:.0f} TFLOP/s  "
+      f"speedup {f2 / f1:.2f}x", flush=True)

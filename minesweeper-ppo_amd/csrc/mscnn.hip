@@ -69,27 +69,40 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
 }
 
-// LDS layout (bf16 elements): sX[(H+2)*(W+2)][CINP] halo tile, sW[COUT][CINP]
-// one tap of weights; then f32 sRed[WAVES][NGRP].
+// LDS layout (bf16 elements):
+//   region0: sX[(H+2)*(W+2)][CINP] zero-halo input tile; after the conv the
+//            same bytes hold sO[P][96] (y staged for the coalesced epilogue);
+//   sW[2][COUT][CINP]: double-buffered weights of one tap;
+//   f32 sRed[WAVES][NGRP], sGB[2][COUT] (gamma, beta).
 template <int CIN>
 constexpr int cinp() { return CIN + 8; }  // +16 B per pixel row: conflict-free ds_read_b128
+
+template <int CIN>
+__host__ __device__ inline int region0_elems(int H, int W) {
+  const int a = (H + 2) * (W + 2) * cinp<CIN>(), b = H * W * COUT;
+  return ((a > b ? a : b) + 7) & ~7;
+}
 
 template <int CIN, int NPT>
 __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int CINP = cinp<CIN>();
+  constexpr int C8 = CIN / 8;
+  constexpr int NPF = (NPT * 128 * C8 + 255) / 256;  // 16-B input chunks per thread
+  constexpr int NWC = (COUT * C8 + 255) / 256;        // 16-B weight chunks per thread and tap
   const int H = p.H, W = p.W, P = H * W, WP = W + 2;
+  const int nhalo = (H + 2) * WP;
   __bf16* sX = reinterpret_cast<__bf16*>(smem);
-  __bf16* sW = sX + (H + 2) * WP * CINP;
-  float* sRed = reinterpret_cast<float*>(sW + COUT * CINP);
+  __bf16* sO = sX;
+  __bf16* sW = sX + region0_elems<CIN>(H, W);
+  float* sRed = reinterpret_cast<float*>(sW + 2 * COUT * CINP);
+  float* sGB = sRed + WAVES * NGRP;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
 
-  // zero the halo tile once: the border is never overwritten
-  {
-    uint4* z = reinterpret_cast<uint4*>(sX);
-    const int nz = (H + 2) * WP * CINP / 8;
-    for (int i = tid; i < nz; i += 256) z[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (int i = tid; i < COUT; i += 256) {
+    sGB[i] = p.gamma[i];
+    sGB[COUT + i] = p.beta[i];
   }
   int aoff[NPT];
   bool aval[NPT];
@@ -100,18 +113,67 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
     const int r = aval[t] ? px / W : 0, c = aval[t] ? px - r * W : 0;
     aoff[t] = ((r + 1) * WP + (c + 1)) * CINP + 8 * hh;
   }
-
-  for (int n = blockIdx.x; n < p.N; n += gridDim.x) {
-    __syncthreads();  // previous sample's epilogue is done with sX/sRed
-    {  // input tile -> LDS interior
-      const uint4* xs = reinterpret_cast<const uint4*>(p.x + (size_t)n * P * CIN);
-      constexpr int C8 = CIN / 8;
-      for (int i = tid; i < P * C8; i += 256) {
-        const int px = i / C8, c8 = i - px * C8;
-        const int r = px / W, c = px - r * W;
-        *reinterpret_cast<uint4*>(&sX[((r + 1) * WP + c + 1) * CINP + c8 * 8]) = xs[i];
+  auto load_in = [&](int n, uint4 (&v)[NPF]) {
+    const uint4* xs = reinterpret_cast<const uint4*>(p.x + (size_t)n * P * CIN);
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) {
+      const int i = tid + 256 * k;
+      if (i < P * C8) v[k] = xs[i];
+    }
+  };
+  auto load_w = [&](int tap, uint4 (&v)[NWC]) {
+    const uint4* ws = reinterpret_cast<const uint4*>(p.wt + (size_t)tap * COUT * CIN);
+#pragma unroll
+    for (int k = 0; k < NWC; ++k) {
+      const int i = tid + 256 * k;
+      if (i < COUT * C8) v[k] = ws[i];
+    }
+  };
+  auto store_w = [&](int buf, const uint4 (&v)[NWC]) {
+    __bf16* d = sW + buf * COUT * CINP;
+#pragma unroll
+    for (int k = 0; k < NWC; ++k) {
+      const int i = tid + 256 * k;
+      if (i < COUT * C8) {
+        const int co = i / C8, c8 = i - co * C8;
+        *reinterpret_cast<uint4*>(&d[co * CINP + c8 * 8]) = v[k];
       }
     }
+  };
+
+  uint4 xin[NPF];
+  uint4 wr[NWC];
+  if (blockIdx.x < p.N) load_in(blockIdx.x, xin);
+  for (int n = blockIdx.x; n < p.N; n += gridDim.x) {
+    // ---- stage input tile (zero halo re-written: the epilogue reuses the region) ----
+    for (int i = tid; i < nhalo - P; i += 256) {  // border cells
+      const int b = i;                             // enumerate border: top, bottom rows, then sides
+      int cell;
+      if (b < WP) cell = b;
+      else if (b < 2 * WP) cell = (H + 1) * WP + (b - WP);
+      else {
+        const int k = b - 2 * WP, r = 1 + (k >> 1);
+        cell = r * WP + ((k & 1) ? WP - 1 : 0);
+      }
+      uint4* d = reinterpret_cast<uint4*>(&sX[cell * CINP]);
+#pragma unroll
+      for (int c8 = 0; c8 < C8; ++c8) d[c8] = make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) {
+      const int i = tid + 256 * k;
+      if (i < P * C8) {
+        const int px = i / C8, c8 = i - px * C8;
+        const int r = px / W, c = px - r * W;
+        *reinterpret_cast<uint4*>(&sX[((r + 1) * WP + c + 1) * CINP + c8 * 8]) = xin[k];
+      }
+    }
+    load_w(0, wr);
+    store_w(0, wr);
+    const int nn = n + gridDim.x;
+    if (nn < p.N) load_in(nn, xin);  // prefetch the next sample under this one's MFMAs
+    __syncthreads();
+
     f32x16 acc[NPT][3];
 #pragma unroll
     for (int t = 0; t < NPT; ++t)
@@ -121,16 +183,8 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
         for (int i = 0; i < 16; ++i) acc[t][ct][i] = 0.f;
 
     for (int tap = 0; tap < 9; ++tap) {
-      __syncthreads();  // sW free (previous tap done); sX writes visible
-      {
-        const uint4* ws = reinterpret_cast<const uint4*>(p.wt + (size_t)tap * COUT * CIN);
-        constexpr int C8 = CIN / 8;
-        for (int i = tid; i < COUT * C8; i += 256) {
-          const int co = i / C8, c8 = i - co * C8;
-          *reinterpret_cast<uint4*>(&sW[co * CINP + c8 * 8]) = ws[i];
-        }
-      }
-      __syncthreads();
+      if (tap + 1 < 9) load_w(tap + 1, wr);
+      const __bf16* sWt = sW + (tap & 1) * COUT * CINP;
       const int dr = tap / 3 - 1, dc = tap % 3 - 1;
       const int tshift = (dr * WP + dc) * CINP;
 #pragma unroll
@@ -138,7 +192,7 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
         bf16x8 b[3];
 #pragma unroll
         for (int ct = 0; ct < 3; ++ct)
-          b[ct] = *reinterpret_cast<const bf16x8*>(&sW[(ct * 32 + l32) * CINP + k0 + 8 * hh]);
+          b[ct] = *reinterpret_cast<const bf16x8*>(&sWt[(ct * 32 + l32) * CINP + k0 + 8 * hh]);
 #pragma unroll
         for (int t = 0; t < NPT; ++t) {
           bf16x8 a = *reinterpret_cast<const bf16x8*>(&sX[aoff[t] + tshift + k0]);
@@ -147,18 +201,21 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
           for (int ct = 0; ct < 3; ++ct) acc[t][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[ct], acc[t][ct], 0, 0, 0);
         }
       }
+      if (tap + 1 < 9) store_w((tap + 1) & 1, wr);  // that buffer was last read in tap-1
+      __syncthreads();
     }
 
-    // ---------------- epilogue: bias, GroupNorm, residual, ReLU, dropout ----------------
+    // ---------------- epilogue A: bias, GroupNorm statistics, y -> LDS ----------------
     float biasv[3];
 #pragma unroll
     for (int ct = 0; ct < 3; ++ct) biasv[ct] = p.bias[ct * 32 + l32];
-    float mean[3], rstd[3];  // this lane's group statistics, per co tile
+    float gmean[NGRP], grstd[NGRP];
     const float inv_cnt = 1.0f / (16.0f * (float)P);
     for (int pass = 0; pass < 2; ++pass) {
       float part[3];
 #pragma unroll
       for (int ct = 0; ct < 3; ++ct) {
+        const float mu = pass ? gmean[2 * ct + (l32 >> 4)] : 0.f;
         float s = 0.f;
 #pragma unroll
         for (int t = 0; t < NPT; ++t)
@@ -166,23 +223,18 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
           for (int i = 0; i < 16; ++i) {
             const int px = (wave * NPT + t) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
             if (px < P) {
-              const float v = acc[t][ct][i] + biasv[ct];
-              s += pass == 0 ? v : (v - mean[ct]) * (v - mean[ct]);
+              const float d = acc[t][ct][i] + biasv[ct] - mu;
+              s += pass ? d * d : d;
             }
           }
         part[ct] = row_sum16(s);
       }
-      // rows 0/2 (lanes 0-15, 32-47) hold channels ct*32+0..15 = group 2ct, rows
-      // 1/3 group 2ct+1. The readlanes stay in converged control flow: inside a
-      // lane-0 branch the compiler may sink the last DPP add into the branch and
-      // the readlane would see the other lanes' stale values.
-      float gs[3][2];
+      float gs[3][2];  // readlanes in converged control flow (see note in the stats exchange)
 #pragma unroll
       for (int ct = 0; ct < 3; ++ct) {
         gs[ct][0] = readlane_f(part[ct], 15) + readlane_f(part[ct], 47);
         gs[ct][1] = readlane_f(part[ct], 31) + readlane_f(part[ct], 63);
       }
-      __syncthreads();  // sRed reuse across passes
       if (lane == 0) {
 #pragma unroll
         for (int ct = 0; ct < 3; ++ct) {
@@ -192,55 +244,74 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
       }
       __syncthreads();
 #pragma unroll
-      for (int ct = 0; ct < 3; ++ct) {
-        const int g = 2 * ct + (l32 >> 4);
+      for (int g = 0; g < NGRP; ++g) {
         float tot = 0.f;
 #pragma unroll
         for (int w = 0; w < WAVES; ++w) tot += sRed[w * NGRP + g];
-        if (pass == 0) {
-          mean[ct] = tot * inv_cnt;
-        } else {
-          rstd[ct] = rsqrtf(tot * inv_cnt + p.eps);
+        if (pass == 0) gmean[g] = tot * inv_cnt;
+        else grstd[g] = rsqrtf(tot * inv_cnt + p.eps);
+      }
+      __syncthreads();  // sRed reused by the next pass
+    }
+    if (p.stats && tid < NGRP) {
+      float m = 0.f, r = 0.f;
+#pragma unroll
+      for (int g = 0; g < NGRP; ++g)
+        if (g == tid) {
+          m = gmean[g];
+          r = grstd[g];
         }
-      }
-    }
-    if (p.stats && wave == 0 && (l32 & 15) == 0 && hh == 0) {
-#pragma unroll
-      for (int ct = 0; ct < 3; ++ct) {
-        const int g = 2 * ct + (l32 >> 4);
-        p.stats[((size_t)n * NGRP + g) * 2 + 0] = mean[ct];
-        p.stats[((size_t)n * NGRP + g) * 2 + 1] = rstd[ct];
-      }
+      p.stats[((size_t)n * NGRP + tid) * 2 + 0] = m;
+      p.stats[((size_t)n * NGRP + tid) * 2 + 1] = r;
     }
 #pragma unroll
-    for (int ct = 0; ct < 3; ++ct) {
-      const int co = ct * 32 + l32;
-      const float ga = p.gamma[co] * rstd[ct];
-      const float be = p.beta[co] - mean[ct] * ga;
-      const float dm = p.dmask ? p.dmask[(size_t)n * COUT + co] : 1.0f;
+    for (int ct = 0; ct < 3; ++ct)
 #pragma unroll
       for (int t = 0; t < NPT; ++t)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int px = (wave * NPT + t) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          if (px < P) {
-            const size_t o = ((size_t)n * P + px) * COUT + co;
-            const float v = acc[t][ct][i] + biasv[ct];
-            float z = v * ga + be;
-            if (p.res) z += (float)p.res[o];
-            z = fmaxf(z, 0.f) * dm;
-            p.out[o] = (__bf16)z;
-            if (p.ysave) p.ysave[o] = (__bf16)v;
-          }
+          if (px < P) sO[px * COUT + ct * 32 + l32] = (__bf16)(acc[t][ct][i] + biasv[ct]);
         }
+    __syncthreads();
+
+    // ---------------- epilogue B: coalesced 16-B chunks of [px][co] ----------------
+    for (int c = tid; c < P * (COUT / 8); c += 256) {
+      const int px = c / (COUT / 8), c8 = c - px * (COUT / 8);
+      const int co0 = c8 * 8, g = c8 >> 1;
+      const size_t o = ((size_t)n * P + px) * COUT + co0;
+      const uint4 yv = *reinterpret_cast<const uint4*>(&sO[px * COUT + co0]);
+      if (p.ysave) *reinterpret_cast<uint4*>(&p.ysave[o]) = yv;
+      float mu = 0.f, rs = 0.f;
+#pragma unroll
+      for (int gg = 0; gg < NGRP; ++gg)
+        if (gg == g) {
+          mu = gmean[gg];
+          rs = grstd[gg];
+        }
+      const bf16x8 y8 = __builtin_bit_cast(bf16x8, yv);
+      bf16x8 r8 = bf16x8{};
+      if (p.res) r8 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(&p.res[o]));
+      bf16x8 o8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int co = co0 + j;
+        float z = ((float)y8[j] - mu) * rs * sGB[co] + sGB[COUT + co] + (float)r8[j];
+        z = fmaxf(z, 0.f);
+        if (p.dmask) z *= p.dmask[(size_t)n * COUT + co];
+        o8[j] = (__bf16)z;
+      }
+      *reinterpret_cast<uint4*>(&p.out[o]) = __builtin_bit_cast(uint4, o8);
     }
+    __syncthreads();  // region0 is re-staged with the next input
   }
 }
 
 template <int CIN, int NPT>
 int launch_fwd(const FwdParams& p, hipStream_t s) {
   constexpr int CINP = cinp<CIN>();
-  const size_t lds = (size_t)(p.H + 2) * (p.W + 2) * CINP * 2 + (size_t)COUT * CINP * 2 + WAVES * NGRP * 4;
+  const size_t lds = (size_t)region0_elems<CIN>(p.H, p.W) * 2 + (size_t)2 * COUT * CINP * 2 + WAVES * NGRP * 4 +
+                     2 * COUT * 4;
   if (lds > 160 * 1024) {
     snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd: board %dx%d needs %zu B LDS", p.H, p.W, lds);
     return MS_EINVAL;

@@ -83,7 +83,7 @@ __host__ __device__ inline int region0_elems(int H, int W) {
   return ((a > b ? a : b) + 7) & ~7;
 }
 
-template <int CIN, int NPT>
+template <int CIN, int NPT, bool FULL>
 __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int CINP = cinp<CIN>();
@@ -96,7 +96,8 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
   __bf16* sO = sX;
   __bf16* sW = sX + region0_elems<CIN>(H, W);
   float* sRed = reinterpret_cast<float*>(sW + 2 * COUT * CINP);
-  float* sGB = sRed + WAVES * NGRP;
+  float* sGB = sRed + WAVES * NGRP;  // [gamma | beta]
+  float* sAB = sGB + 2 * COUT;        // per sample: [scale | shift | dropout scale]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
 
@@ -171,7 +172,6 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
     load_w(0, wr);
     store_w(0, wr);
     const int nn = n + gridDim.x;
-    if (nn < p.N) load_in(nn, xin);  // prefetch the next sample under this one's MFMAs
     __syncthreads();
 
     f32x16 acc[NPT][3];
@@ -183,7 +183,10 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
         for (int i = 0; i < 16; ++i) acc[t][ct][i] = 0.f;
 
     for (int tap = 0; tap < 9; ++tap) {
+      // vmcnt retires loads in issue order: the next sample's (HBM) input prefetch is
+      // issued on the last tap so no weight-tap wait ever queues behind it
       if (tap + 1 < 9) load_w(tap + 1, wr);
+      else if (nn < p.N) load_in(nn, xin);
       const __bf16* sWt = sW + (tap & 1) * COUT * CINP;
       const int dr = tap / 3 - 1, dc = tap % 3 - 1;
       const int tshift = (dr * WP + dc) * CINP;
@@ -196,7 +199,7 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
 #pragma unroll
         for (int t = 0; t < NPT; ++t) {
           bf16x8 a = *reinterpret_cast<const bf16x8*>(&sX[aoff[t] + tshift + k0]);
-          if (!aval[t]) a = bf16x8{};
+          if (!FULL && !aval[t]) a = bf16x8{};
 #pragma unroll
           for (int ct = 0; ct < 3; ++ct) acc[t][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[ct], acc[t][ct], 0, 0, 0);
         }
@@ -271,17 +274,10 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int px = (wave * NPT + t) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          if (px < P) sO[px * COUT + ct * 32 + l32] = (__bf16)(acc[t][ct][i] + biasv[ct]);
+          if (FULL || px < P) sO[px * COUT + ct * 32 + l32] = (__bf16)(acc[t][ct][i] + biasv[ct]);
         }
-    __syncthreads();
-
-    // ---------------- epilogue B: coalesced 16-B chunks of [px][co] ----------------
-    for (int c = tid; c < P * (COUT / 8); c += 256) {
-      const int px = c / (COUT / 8), c8 = c - px * (COUT / 8);
-      const int co0 = c8 * 8, g = c8 >> 1;
-      const size_t o = ((size_t)n * P + px) * COUT + co0;
-      const uint4 yv = *reinterpret_cast<const uint4*>(&sO[px * COUT + co0]);
-      if (p.ysave) *reinterpret_cast<uint4*>(&p.ysave[o]) = yv;
+    if (tid < COUT) {  // z = y * scale + shift (+ res), then ReLU, then * dropout scale
+      const int g = tid >> 4;
       float mu = 0.f, rs = 0.f;
 #pragma unroll
       for (int gg = 0; gg < NGRP; ++gg)
@@ -289,6 +285,20 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
           mu = gmean[gg];
           rs = grstd[gg];
         }
+      const float a = sGB[tid] * rs;
+      sAB[tid] = a;
+      sAB[COUT + tid] = sGB[COUT + tid] - mu * a;
+      sAB[2 * COUT + tid] = p.dmask ? p.dmask[(size_t)n * COUT + tid] : 1.0f;
+    }
+    __syncthreads();
+
+    // ---------------- epilogue B: coalesced 16-B chunks of [px][co] ----------------
+    for (int c = tid; c < P * (COUT / 8); c += 256) {
+      const int px = c / (COUT / 8), c8 = c - px * (COUT / 8);
+      const int co0 = c8 * 8;
+      const size_t o = ((size_t)n * P + px) * COUT + co0;
+      const uint4 yv = *reinterpret_cast<const uint4*>(&sO[px * COUT + co0]);
+      if (p.ysave) *reinterpret_cast<uint4*>(&p.ysave[o]) = yv;
       const bf16x8 y8 = __builtin_bit_cast(bf16x8, yv);
       bf16x8 r8 = bf16x8{};
       if (p.res) r8 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(&p.res[o]));
@@ -296,10 +306,8 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int co = co0 + j;
-        float z = ((float)y8[j] - mu) * rs * sGB[co] + sGB[COUT + co] + (float)r8[j];
-        z = fmaxf(z, 0.f);
-        if (p.dmask) z *= p.dmask[(size_t)n * COUT + co];
-        o8[j] = (__bf16)z;
+        const float z = fmaxf((float)y8[j] * sAB[co] + sAB[COUT + co] + (float)r8[j], 0.f);
+        o8[j] = (__bf16)(z * sAB[2 * COUT + co]);
       }
       *reinterpret_cast<uint4*>(&p.out[o]) = __builtin_bit_cast(uint4, o8);
     }
@@ -307,18 +315,18 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
   }
 }
 
-template <int CIN, int NPT>
+template <int CIN, int NPT, bool FULL>
 int launch_fwd(const FwdParams& p, hipStream_t s) {
   constexpr int CINP = cinp<CIN>();
   const size_t lds = (size_t)region0_elems<CIN>(p.H, p.W) * 2 + (size_t)2 * COUT * CINP * 2 + WAVES * NGRP * 4 +
-                     2 * COUT * 4;
+                     5 * COUT * 4;
   if (lds > 160 * 1024) {
     snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd: board %dx%d needs %zu B LDS", p.H, p.W, lds);
     return MS_EINVAL;
   }
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k_conv_gn_fwd<CIN, NPT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)k_conv_gn_fwd<CIN, NPT, FULL>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     attr_set = true;
   }
@@ -326,7 +334,7 @@ int launch_fwd(const FwdParams& p, hipStream_t s) {
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   const int grid = p.N < ncu ? p.N : ncu;
-  hipLaunchKernelGGL((k_conv_gn_fwd<CIN, NPT>), dim3(grid), dim3(256), lds, s, p);
+  hipLaunchKernelGGL((k_conv_gn_fwd<CIN, NPT, FULL>), dim3(grid), dim3(256), lds, s, p);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd launch: %s", hipGetErrorString(e));
@@ -340,11 +348,12 @@ int dispatch_fwd(const FwdParams& p, hipStream_t s) {
   const int P = p.H * p.W;
   const int tiles = (P + 31) / 32;
   const int npt = (tiles + WAVES - 1) / WAVES;
+  if (P == 256) return launch_fwd<CIN, 2, true>(p, s);  // 16x16: every 32-px tile is full
   switch (npt) {
-    case 1: return launch_fwd<CIN, 1>(p, s);
-    case 2: return launch_fwd<CIN, 2>(p, s);
-    case 3: return launch_fwd<CIN, 3>(p, s);
-    case 4: return launch_fwd<CIN, 4>(p, s);
+    case 1: return launch_fwd<CIN, 1, false>(p, s);
+    case 2: return launch_fwd<CIN, 2, false>(p, s);
+    case 3: return launch_fwd<CIN, 3, false>(p, s);
+    case 4: return launch_fwd<CIN, 4, false>(p, s);
     default:
       snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd: %d pixels > 512 unsupported", P);
       return MS_EINVAL;

@@ -29,6 +29,7 @@ namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // native vector: HIP's uint4 struct copies via memcpy and stays in scratch
 
 constexpr int COUT = 96;
 constexpr int NGRP = 6;  // GroupNorm groups (96 / 16)
@@ -83,6 +84,35 @@ __host__ __device__ inline int region0_elems(int H, int W) {
   return ((a > b ? a : b) + 7) & ~7;
 }
 
+// (macros rather than lambdas: captured register arrays would be demoted to scratch)
+#define MC_LOAD_IN(n_, v_)                                                              \
+  do {                                                                                  \
+    const u32x4* xs_ = reinterpret_cast<const u32x4*>(p.x + (size_t)(n_) * P * CIN);   \
+    _Pragma("unroll") for (int k_ = 0; k_ < NPF; ++k_) {                                \
+      const int i_ = tid + 256 * k_;                                                    \
+      if (i_ < P * C8) v_[k_] = xs_[i_];                                                \
+    }                                                                                   \
+  } while (0)
+#define MC_LOAD_W(tap_, v_)                                                             \
+  do {                                                                                  \
+    const u32x4* ws_ = reinterpret_cast<const u32x4*>(p.wt + (size_t)(tap_) * COUT * CIN); \
+    _Pragma("unroll") for (int k_ = 0; k_ < NWC; ++k_) {                                \
+      const int i_ = tid + 256 * k_;                                                    \
+      if (i_ < COUT * C8) v_[k_] = ws_[i_];                                             \
+    }                                                                                   \
+  } while (0)
+#define MC_STORE_W(buf_, v_)                                                            \
+  do {                                                                                  \
+    __bf16* d_ = sW + (buf_) * COUT * CINP;                                             \
+    _Pragma("unroll") for (int k_ = 0; k_ < NWC; ++k_) {                                \
+      const int i_ = tid + 256 * k_;                                                    \
+      if (i_ < COUT * C8) {                                                             \
+        const int co_ = i_ / C8, c8_ = i_ - co_ * C8;                                   \
+        *reinterpret_cast<u32x4*>(&d_[co_ * CINP + c8_ * 8]) = v_[k_];                  \
+      }                                                                                 \
+    }                                                                                   \
+  } while (0)
+
 template <int CIN, int NPT, bool FULL>
 __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -114,37 +144,9 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
     const int r = aval[t] ? px / W : 0, c = aval[t] ? px - r * W : 0;
     aoff[t] = ((r + 1) * WP + (c + 1)) * CINP + 8 * hh;
   }
-  auto load_in = [&](int n, uint4 (&v)[NPF]) {
-    const uint4* xs = reinterpret_cast<const uint4*>(p.x + (size_t)n * P * CIN);
-#pragma unroll
-    for (int k = 0; k < NPF; ++k) {
-      const int i = tid + 256 * k;
-      if (i < P * C8) v[k] = xs[i];
-    }
-  };
-  auto load_w = [&](int tap, uint4 (&v)[NWC]) {
-    const uint4* ws = reinterpret_cast<const uint4*>(p.wt + (size_t)tap * COUT * CIN);
-#pragma unroll
-    for (int k = 0; k < NWC; ++k) {
-      const int i = tid + 256 * k;
-      if (i < COUT * C8) v[k] = ws[i];
-    }
-  };
-  auto store_w = [&](int buf, const uint4 (&v)[NWC]) {
-    __bf16* d = sW + buf * COUT * CINP;
-#pragma unroll
-    for (int k = 0; k < NWC; ++k) {
-      const int i = tid + 256 * k;
-      if (i < COUT * C8) {
-        const int co = i / C8, c8 = i - co * C8;
-        *reinterpret_cast<uint4*>(&d[co * CINP + c8 * 8]) = v[k];
-      }
-    }
-  };
-
-  uint4 xin[NPF];
-  uint4 wr[NWC];
-  if (blockIdx.x < p.N) load_in(blockIdx.x, xin);
+  u32x4 xin[NPF];
+  u32x4 wr[NWC];
+  if ((int)blockIdx.x < p.N) MC_LOAD_IN(blockIdx.x, xin);
   for (int n = blockIdx.x; n < p.N; n += gridDim.x) {
     // ---- stage input tile (zero halo re-written: the epilogue reuses the region) ----
     for (int i = tid; i < nhalo - P; i += 256) {  // border cells
@@ -166,11 +168,11 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
       if (i < P * C8) {
         const int px = i / C8, c8 = i - px * C8;
         const int r = px / W, c = px - r * W;
-        *reinterpret_cast<uint4*>(&sX[((r + 1) * WP + c + 1) * CINP + c8 * 8]) = xin[k];
+        *reinterpret_cast<u32x4*>(&sX[((r + 1) * WP + c + 1) * CINP + c8 * 8]) = xin[k];
       }
     }
-    load_w(0, wr);
-    store_w(0, wr);
+    MC_LOAD_W(0, wr);
+    MC_STORE_W(0, wr);
     const int nn = n + gridDim.x;
     __syncthreads();
 
@@ -185,8 +187,8 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
     for (int tap = 0; tap < 9; ++tap) {
       // vmcnt retires loads in issue order: the next sample's (HBM) input prefetch is
       // issued on the last tap so no weight-tap wait ever queues behind it
-      if (tap + 1 < 9) load_w(tap + 1, wr);
-      else if (nn < p.N) load_in(nn, xin);
+      if (tap + 1 < 9) MC_LOAD_W(tap + 1, wr);
+      else if (nn < p.N) MC_LOAD_IN(nn, xin);
       const __bf16* sWt = sW + (tap & 1) * COUT * CINP;
       const int dr = tap / 3 - 1, dc = tap % 3 - 1;
       const int tshift = (dr * WP + dc) * CINP;
@@ -204,7 +206,7 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
           for (int ct = 0; ct < 3; ++ct) acc[t][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[ct], acc[t][ct], 0, 0, 0);
         }
       }
-      if (tap + 1 < 9) store_w((tap + 1) & 1, wr);  // that buffer was last read in tap-1
+      if (tap + 1 < 9) MC_STORE_W((tap + 1) & 1, wr);  // that buffer was last read in tap-1
       __syncthreads();
     }
 

@@ -31,6 +31,31 @@ int mc_conv_gn_fwd(const uint16_t* x, const uint16_t* w, const float* bias, cons
                    uint16_t* ysave, float* stats, int32_t n, int32_t h, int32_t w_, int32_t cin,
                    float eps, void* stream);
 
+/* Backward of one fused layer (the forward above with the same n, h, w, cin).
+ * Inputs: dout = dL/d(out); out, ysave, stats from the forward; x = the forward's
+ * input; wT = the conv weight re-laid out as bf16 [9][cin][96] (tap, ci, co), or
+ * NULL when no input gradient is wanted (the stem: its input is the observation).
+ * addend (bf16 [N][P][cin], may be NULL) is added to dx (the block input's skip
+ * gradient). Outputs:
+ *   dy     bf16 [N][P][96]  dL/dy, the conv-output gradient (also a workspace);
+ *   dz     bf16 [N][P][96]  dL/d(pre-ReLU sum) = the residual gradient, or NULL;
+ *   dx     bf16 [N][P][cin] conv input gradient (+ addend), NULL iff wT is NULL;
+ *   dw     f32 [9][96][cin] weight gradient (tap, co, ci);
+ *   dgn    f32 [3][96]      d gamma, d beta, d bias.
+ * work: f32 scratch of at least mc_conv_gn_bwd_workspace(...) floats.
+ * Replaces autograd through cnn_residual.py:10-26, 50-54 (conv/GN/ReLU/Dropout2d). */
+int mc_conv_gn_bwd(const uint16_t* dout, const uint16_t* out, const uint16_t* ysave, const float* stats,
+                   const float* gamma, const float* dmask, const uint16_t* x, const uint16_t* wT,
+                   const uint16_t* addend, uint16_t* dy, uint16_t* dz, uint16_t* dx, float* dw, float* dgn,
+                   float* work, int64_t work_floats, int32_t n, int32_t h, int32_t w_, int32_t cin,
+                   void* stream);
+
+/* f32 elements of scratch mc_conv_gn_bwd needs for these sizes. */
+int64_t mc_conv_gn_bwd_workspace(int32_t n, int32_t h, int32_t w_, int32_t cin);
+
+/* Thread-local message of the last failing mc_* call. */
+const char* mc_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif

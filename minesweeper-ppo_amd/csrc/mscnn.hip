@@ -24,18 +24,28 @@
 
 #include "../../include/msenv.h"
 #include "../../include/mscnn.h"
+#include "mscnn_common.h"
+
+namespace mc {
+
+thread_local char g_err[256] = "";
+
+int num_cus() {
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0, v = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+    ncu = v > 0 ? v : 256;
+  }
+  return ncu;
+}
+
+}  // namespace mc
 
 namespace {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // native vector: HIP's uint4 struct copies via memcpy and stays in scratch
-
-constexpr int COUT = 96;
-constexpr int NGRP = 6;  // GroupNorm groups (96 / 16)
-constexpr int WAVES = 4;
-
-thread_local char g_err[256] = "";
+using namespace mc;
 
 struct FwdParams {
   const __bf16* x;
@@ -51,24 +61,6 @@ struct FwdParams {
   int N, H, W;
   float eps;
 };
-
-template <int CTRL>
-__device__ __forceinline__ float dppf(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, true));
-}
-
-// sum over each 16-lane row; the result is valid in lanes 15, 31, 47, 63
-__device__ __forceinline__ float row_sum16(float v) {
-  v += dppf<0x111>(v);
-  v += dppf<0x112>(v);
-  v += dppf<0x114>(v);
-  v += dppf<0x118>(v);
-  return v;
-}
-
-__device__ __forceinline__ float readlane_f(float v, int l) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
-}
 
 // LDS layout (bf16 elements):
 //   region0: sX[(H+2)*(W+2)][CINP] zero-halo input tile; after the conv the
@@ -332,9 +324,7 @@ int launch_fwd(const FwdParams& p, hipStream_t s) {
                               160 * 1024);
     attr_set = true;
   }
-  int dev = 0, ncu = 256;
-  (void)hipGetDevice(&dev);
-  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const int ncu = num_cus();
   const int grid = p.N < ncu ? p.N : ncu;
   hipLaunchKernelGGL((k_conv_gn_fwd<CIN, NPT, FULL>), dim3(grid), dim3(256), lds, s, p);
   const hipError_t e = hipGetLastError();

@@ -1,0 +1,594 @@
+// mscnn_bwd.hip — backward of the fused residual-CNN layer (gfx950 MFMA).
+//
+// Forward (mscnn.hip, reference chain minesweeper/models/cnn_residual.py:10-26, 50-54):
+//   y = conv3x3(x, w) + bias;  z = GN(y) * gamma + beta [+ res];  out = relu(z) [* dmask]
+// Backward, per layer, in two persistent kernels:
+//   k_bwd_data  (one workgroup per sample at a time, 2 workgroups per CU)
+//     pass 1: dz = (out > 0) * dout * dmask  and the per-channel sums
+//             S1 = sum dz, S2 = sum dz*yhat, S3 = sum yhat (yhat = (y - mean) * rstd);
+//     pass 2: dy = rstd*gamma*dz - rstd*mean_g(gamma*dz) - rstd*yhat*mean_g(gamma*dz*yhat)
+//             (GroupNorm backward), kept in an LDS tile and stored for k_wgrad;
+//     dgrad : dx[q] = sum_tap dy[q - s(tap)] . W[tap]^T on v_mfma_f32_32x32x16_bf16
+//             (A = 32 pixels x 16 co read from the dy tile by per-lane shifted row
+//             addresses, out-of-board rows pointing at a zero row; B = W^T[tap] [ci][co]),
+//             + the skip-gradient addend, one bf16 store.
+//     d gamma = sum S2, d beta = sum S1, d bias = sum dy come out of the same sums.
+//   k_wgrad (XCD-aware grid: the 3 workgroups that split ci of one sample group sit on
+//            one XCD so the dy they all read is shared in its L2)
+//     dW[tap][co][ci] = sum_{n,p} dy[n][p][co] * x[n][p + s(tap)][ci]: a GEMM whose K is
+//     every pixel of every sample; both operands are read K-major with
+//     ds_read_b64_tr_b16 straight from the NHWC tiles (dy [P][96], x [halo][32]).
+// Per-workgroup partials are summed by k_reduce (deterministic, no atomics).
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../../include/msenv.h"
+#include "../../include/mscnn.h"
+#include "mscnn_common.h"
+
+namespace {
+
+using namespace mc;
+
+constexpr int DCP = 104;       // dy tile row stride (elements): conflict-free ds_read_b128 row reads
+constexpr int PG = 21;         // pixel groups of the element-wise passes: thread = (pg, c8)
+constexpr int NC8 = COUT / 8;  // 16-byte chunks per 96-channel pixel row
+
+struct BwdDataParams {
+  const __bf16* dout;
+  const __bf16* out;
+  const __bf16* y;
+  const float* stats;
+  const float* gamma;
+  const float* dmask;
+  const __bf16* wT;
+  const __bf16* addend;
+  __bf16* dy;
+  __bf16* dz;
+  __bf16* dx;
+  float* part;  // [gridDim][3][96]
+  int N, H, W;
+};
+
+__host__ __device__ inline int dtile_bytes(int P) { return ((P + 1) * DCP * 2 + 15) & ~15; }
+__host__ __device__ constexpr int red_bytes() {  // sRed [PG][3][96] f32, aliased by sW [96][DCP] bf16
+  return PG * 3 * COUT * 4 > COUT * DCP * 2 ? PG * 3 * COUT * 4 : COUT * DCP * 2;
+}
+__host__ __device__ inline int bwd_data_lds(int P) { return dtile_bytes(P) + red_bytes() + 6 * COUT * 4; }
+
+template <int NPT, bool DGRAD, int NCH>
+__global__ __launch_bounds__(256, 2) void k_bwd_data(BwdDataParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int H = p.H, W = p.W, P = H * W;
+  __bf16* sD = reinterpret_cast<__bf16*>(smem);  // [P+1][DCP] (row P = 0); later [P][96] dx staging
+  float* sRed = reinterpret_cast<float*>(smem + dtile_bytes(P));
+  __bf16* sW = reinterpret_cast<__bf16*>(sRed);  // W^T[tap] as [ci][DCP]
+  float* sCo = reinterpret_cast<float*>(smem + dtile_bytes(P) + red_bytes());  // [3][96]
+  float* sTmp = sCo + 3 * COUT;                                                 // [2][96]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hh = lane >> 5;
+  const int pg = tid / NC8, c8 = tid - pg * NC8;
+  const bool gact = tid < PG * NC8;
+  const int grp = c8 >> 1;
+  const float inv_cnt = 1.0f / (16.0f * (float)P);
+  float acc_g = 0.f, acc_b = 0.f, acc_bias = 0.f;  // tid < 96: running sums for channel tid
+
+  for (int i = tid; i < DCP / 8; i += 256) *reinterpret_cast<u32x4*>(&sD[P * DCP + 8 * i]) = u32x4{0u, 0u, 0u, 0u};
+  int qr[NPT], qc[NPT];
+#pragma unroll
+  for (int t = 0; t < NPT; ++t) {
+    const int q = (wave * NPT + t) * 32 + l32;
+    qr[t] = q < P ? q / W : -1000;  // an invalid pixel never lands on the board
+    qc[t] = q < P ? q - qr[t] * W : -1000;
+  }
+
+  for (int n = blockIdx.x; n < p.N; n += gridDim.x) {
+    // ---------------- pass 1: dz and per-channel sums ----------------
+    float dm[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dm[j] = 1.f;
+    float mean = 0.f, rstd = 0.f;
+    if (gact) {
+      if (p.dmask) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dm[j] = p.dmask[(size_t)n * COUT + c8 * 8 + j];
+      }
+      mean = p.stats[((size_t)n * NGRP + grp) * 2];
+      rstd = p.stats[((size_t)n * NGRP + grp) * 2 + 1];
+    }
+    // y stays in registers for pass 2; dz goes to its slot of the dy tile (rewritten in place)
+    u32x4 yr[NCH];
+    float s1[8], s2[8], s3[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s1[j] = s2[j] = s3[j] = 0.f;
+    constexpr int LB = 4;  // chunks whose loads are in flight together
+#pragma unroll
+    for (int i0 = 0; i0 < NCH; i0 += LB) {
+      u32x4 dv[LB], ov[LB];
+#pragma unroll
+      for (int u = 0; u < LB; ++u) {
+        const int i = i0 + u, px = pg + PG * i;
+        if (i < NCH) yr[i] = u32x4{0u, 0u, 0u, 0u};
+        if (i < NCH && gact && px < P) {
+          const size_t o = ((size_t)n * P + px) * COUT + c8 * 8;
+          dv[u] = *reinterpret_cast<const u32x4*>(&p.dout[o]);
+          ov[u] = *reinterpret_cast<const u32x4*>(&p.out[o]);
+          yr[i] = *reinterpret_cast<const u32x4*>(&p.y[o]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < LB; ++u) {
+        const int i = i0 + u, px = pg + PG * i;
+        if (i < NCH && gact && px < P) {
+          const bf16x8 d8 = __builtin_bit_cast(bf16x8, dv[u]), o8 = __builtin_bit_cast(bf16x8, ov[u]);
+          const bf16x8 y8 = __builtin_bit_cast(bf16x8, yr[i]);
+          bf16x8 z8;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float d = (float)d8[j] * dm[j];
+            z8[j] = (__bf16)((float)o8[j] > 0.f ? d : 0.f);
+            const float zf = (float)z8[j];
+            const float yh = ((float)y8[j] - mean) * rstd;
+            s1[j] += zf;
+            s2[j] += zf * yh;
+            s3[j] += yh;
+          }
+          const u32x4 zv = __builtin_bit_cast(u32x4, z8);
+          *reinterpret_cast<u32x4*>(&sD[px * DCP + c8 * 8]) = zv;
+          if (p.dz) *reinterpret_cast<u32x4*>(&p.dz[((size_t)n * P + px) * COUT + c8 * 8]) = zv;
+        }
+      }
+    }
+    if (gact) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sRed[(pg * 3 + 0) * COUT + c8 * 8 + j] = s1[j];
+        sRed[(pg * 3 + 1) * COUT + c8 * 8 + j] = s2[j];
+        sRed[(pg * 3 + 2) * COUT + c8 * 8 + j] = s3[j];
+      }
+    }
+    __syncthreads();
+    float S1 = 0.f, S2 = 0.f, S3 = 0.f, gam = 0.f, cmean = 0.f, crstd = 0.f;
+    if (tid < COUT) {
+      for (int g = 0; g < PG; ++g) {
+        S1 += sRed[(g * 3 + 0) * COUT + tid];
+        S2 += sRed[(g * 3 + 1) * COUT + tid];
+        S3 += sRed[(g * 3 + 2) * COUT + tid];
+      }
+      gam = p.gamma[tid];
+      cmean = p.stats[((size_t)n * NGRP + (tid >> 4)) * 2];
+      crstd = p.stats[((size_t)n * NGRP + (tid >> 4)) * 2 + 1];
+      sTmp[tid] = gam * S1;
+      sTmp[COUT + tid] = gam * S2;
+      acc_g += S2;
+      acc_b += S1;
+    }
+    __syncthreads();
+    if (tid < COUT) {
+      const int g0 = (tid >> 4) * 16;
+      float m1 = 0.f, m2 = 0.f;
+      for (int k = 0; k < 16; ++k) {
+        m1 += sTmp[g0 + k];
+        m2 += sTmp[COUT + g0 + k];
+      }
+      m1 *= inv_cnt;
+      m2 *= inv_cnt;
+      sCo[tid] = crstd * gam;
+      sCo[COUT + tid] = -crstd * crstd * m2;
+      sCo[2 * COUT + tid] = crstd * (crstd * m2 * cmean - m1);
+      acc_bias += crstd * (gam * S1 - (float)P * m1 - m2 * S3);
+    }
+    __syncthreads();
+
+    // ---------------- pass 2: dy (GroupNorm backward) -> LDS tile + HBM ----------------
+    constexpr int NWC = (COUT * NC8 + 255) / 256;  // 16-B chunks of one W^T tap per thread
+    u32x4 wr[NWC];
+    if (DGRAD) {
+#pragma unroll
+      for (int k = 0; k < NWC; ++k) {
+        const int c = tid + 256 * k;
+        if (c < COUT * NC8) wr[k] = reinterpret_cast<const u32x4*>(p.wT)[c];
+      }
+    }
+    if (gact) {
+      float A[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) A[j] = sCo[c8 * 8 + j];
+      const float Bg = sCo[COUT + c8 * 8], Cg = sCo[2 * COUT + c8 * 8];
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        const int px = pg + PG * i;
+        if (px < P) {
+          const bf16x8 z8 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(&sD[px * DCP + c8 * 8]));
+          const bf16x8 y8 = __builtin_bit_cast(bf16x8, yr[i]);
+          bf16x8 d8;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) d8[j] = (__bf16)(A[j] * (float)z8[j] + Bg * (float)y8[j] + Cg);
+          const u32x4 v = __builtin_bit_cast(u32x4, d8);
+          *reinterpret_cast<u32x4*>(&sD[px * DCP + c8 * 8]) = v;
+          *reinterpret_cast<u32x4*>(&p.dy[((size_t)n * P + px) * COUT + c8 * 8]) = v;
+        }
+      }
+    }
+    if (!DGRAD) continue;  // (uniform) the stem's input needs no gradient
+
+#pragma unroll
+    for (int k = 0; k < NWC; ++k) {
+      const int c = tid + 256 * k;
+      if (c < COUT * NC8) {
+        const int ci = c / NC8, k8 = c - ci * NC8;
+        *reinterpret_cast<u32x4*>(&sW[ci * DCP + k8 * 8]) = wr[k];
+      }
+    }
+    __syncthreads();
+
+    // ---------------- dgrad: dx = sum_tap shift(dy) . W^T[tap] ----------------
+    f32x16 acc[NPT][3];
+#pragma unroll
+    for (int t = 0; t < NPT; ++t)
+#pragma unroll
+      for (int ct = 0; ct < 3; ++ct)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[t][ct][i] = 0.f;
+    for (int tap = 0; tap < 9; ++tap) {
+      if (tap + 1 < 9) {
+        const u32x4* ws = reinterpret_cast<const u32x4*>(p.wT + (size_t)(tap + 1) * COUT * COUT);
+#pragma unroll
+        for (int k = 0; k < NWC; ++k) {
+          const int c = tid + 256 * k;
+          if (c < COUT * NC8) wr[k] = ws[c];
+        }
+      }
+      const int dr = tap / 3 - 1, dc = tap % 3 - 1;
+      int aoff[NPT];
+#pragma unroll
+      for (int t = 0; t < NPT; ++t) {
+        const int sr = qr[t] - dr, sc = qc[t] - dc;
+        const bool v = (unsigned)sr < (unsigned)H && (unsigned)sc < (unsigned)W;
+        aoff[t] = (v ? sr * W + sc : P) * DCP + 8 * hh;
+      }
+#pragma unroll
+      for (int k0 = 0; k0 < COUT; k0 += 16) {
+        bf16x8 b[3];
+#pragma unroll
+        for (int ct = 0; ct < 3; ++ct)
+          b[ct] = *reinterpret_cast<const bf16x8*>(&sW[(ct * 32 + l32) * DCP + k0 + 8 * hh]);
+#pragma unroll
+        for (int t = 0; t < NPT; ++t) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sD[aoff[t] + k0]);
+#pragma unroll
+          for (int ct = 0; ct < 3; ++ct) acc[t][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[ct], acc[t][ct], 0, 0, 0);
+        }
+      }
+      __syncthreads();  // sW (and, after the last tap, sD) fully read
+      if (tap + 1 < 9) {
+#pragma unroll
+        for (int k = 0; k < NWC; ++k) {
+          const int c = tid + 256 * k;
+          if (c < COUT * NC8) {
+            const int ci = c / NC8, k8 = c - ci * NC8;
+            *reinterpret_cast<u32x4*>(&sW[ci * DCP + k8 * 8]) = wr[k];
+          }
+        }
+        __syncthreads();
+      }
+    }
+    // ---------------- epilogue: dx (+ addend) via a [P][96] staging image ----------------
+#pragma unroll
+    for (int t = 0; t < NPT; ++t)
+#pragma unroll
+      for (int ct = 0; ct < 3; ++ct)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int px = (wave * NPT + t) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          if (px < P) sD[px * COUT + ct * 32 + l32] = (__bf16)acc[t][ct][i];
+        }
+    __syncthreads();
+    if (gact) {
+      u32x4 ad[NCH];  // all addend loads in flight before the first dependent store
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        const int px = pg + PG * i;
+        ad[i] = u32x4{0u, 0u, 0u, 0u};
+        if (p.addend && px < P) ad[i] = *reinterpret_cast<const u32x4*>(&p.addend[((size_t)n * P + px) * COUT + c8 * 8]);
+      }
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        const int px = pg + PG * i;
+        if (px < P) {
+          const bf16x8 a8 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(&sD[px * COUT + c8 * 8]));
+          const bf16x8 r8 = __builtin_bit_cast(bf16x8, ad[i]);
+          bf16x8 s8;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) s8[j] = (__bf16)((float)a8[j] + (float)r8[j]);
+          *reinterpret_cast<u32x4*>(&p.dx[((size_t)n * P + px) * COUT + c8 * 8]) = __builtin_bit_cast(u32x4, s8);
+        }
+      }
+    }
+    // no trailing barrier: the next sample touches sD / sW only after its reduction barriers
+  }
+  if (tid < COUT) {
+    p.part[((size_t)blockIdx.x * 3 + 0) * COUT + tid] = acc_g;
+    p.part[((size_t)blockIdx.x * 3 + 1) * COUT + tid] = acc_b;
+    p.part[((size_t)blockIdx.x * 3 + 2) * COUT + tid] = acc_bias;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+struct WgradParams {
+  const __bf16* dy;
+  const __bf16* x;
+  float* part;  // [G][9][96][CIN]
+  int N, H, W, G;
+};
+
+__host__ __device__ inline int wgrad_lds(int H, int W) {
+  const int P = H * W, Ppad = (P + 15) & ~15;
+  return Ppad * COUT * 2 + (H + 2) * (W + 2) * 32 * 2;
+}
+
+// One wave's share of the 27 (tap, co-tile) 32x32 tiles of a 32-wide ci slice: tiles
+// [T0, T0+NT) in tap-major order, so a wave touches at most 3 taps.
+template <int CIN, int T0, int NT>
+__device__ __forceinline__ void wgrad_body(const WgradParams& p, __bf16* sDY, __bf16* sX, int gid, int ci0) {
+  constexpr int TAP0 = T0 / 3, TAP1 = (T0 + NT - 1) / 3, NTAP = TAP1 - TAP0 + 1;
+  constexpr int XC = CIN < 32 ? CIN : 32;  // real channels of the slice (the stem's 16 + 16 zero)
+  constexpr int XCH = XC / 8;
+  const int H = p.H, W = p.W, P = H * W, Ppad = (P + 15) & ~15, WP = W + 2;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int col = 16 * (g & 1) + 4 * pp;  // tr-read column of this lane within a 32-wide block
+  const int rowoff = 8 * (g >> 1) + q;    // tr-read row (pixel) offset within a 16-deep k step
+  const float invW = 1.0f / (float)W;
+  int tapoff[NTAP];
+#pragma unroll
+  for (int j = 0; j < NTAP; ++j) {
+    const int tap = TAP0 + j;
+    tapoff[j] = ((tap / 3 - 1) * WP + (tap % 3 - 1)) * 32;
+  }
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+
+  for (int n = gid; n < p.N; n += p.G) {
+    const u32x4* dys = reinterpret_cast<const u32x4*>(p.dy + (size_t)n * P * COUT);
+#pragma unroll 4
+    for (int c = tid; c < P * NC8; c += 256) *reinterpret_cast<u32x4*>(&sDY[c * 8]) = dys[c];
+#pragma unroll 2
+    for (int c = tid; c < P * XCH; c += 256) {
+      const int px = c / XCH, k = c - px * XCH;
+      const int r = px / W, cc = px - r * W;
+      *reinterpret_cast<u32x4*>(&sX[((r + 1) * WP + cc + 1) * 32 + k * 8]) =
+          *reinterpret_cast<const u32x4*>(&p.x[((size_t)n * P + px) * CIN + ci0 + k * 8]);
+    }
+    __syncthreads();
+    for (int k0 = 0; k0 < Ppad; k0 += 16) {
+      bf16x8 a[3];
+#pragma unroll
+      for (int cot = 0; cot < 3; ++cot) {
+        const __bf16* base = sDY + (k0 + rowoff) * COUT + cot * 32 + col;
+        a[cot] = cat8(lds_tr4(base), lds_tr4(base + 4 * COUT));
+      }
+      int h[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int px = k0 + rowoff + 4 * s;
+        const int r = (int)(((float)px + 0.5f) * invW);
+        h[s] = px < P ? (r + 1) * WP + (px - r * W) + 1 : W + 3;  // beyond P: dy rows are 0
+      }
+      bf16x8 b[NTAP];
+#pragma unroll
+      for (int j = 0; j < NTAP; ++j)
+        b[j] = cat8(lds_tr4(sX + h[0] * 32 + tapoff[j] + col), lds_tr4(sX + h[1] * 32 + tapoff[j] + col));
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int tt = T0 + t;
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[tt % 3], b[tt / 3 - TAP0], acc[t], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int tt = T0 + t, tap = tt / 3, cot = tt % 3;
+    const int ci = lane & 31;
+    if (ci < XC) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = cot * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        p.part[(((size_t)gid * 9 + tap) * COUT + co) * CIN + ci0 + ci] = acc[t][r];
+      }
+    }
+  }
+}
+
+template <int CIN>
+__global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NCI = CIN / 32 > 0 ? CIN / 32 : 1;
+  const int P = p.H * p.W, Ppad = (P + 15) & ~15;
+  __bf16* sDY = reinterpret_cast<__bf16*>(smem);  // [Ppad][96], rows >= P zero
+  __bf16* sX = sDY + Ppad * COUT;                  // [(H+2)(W+2)][32] zero-halo ci slice
+  const int tid = threadIdx.x;
+  for (int i = P * NC8 + tid; i < Ppad * NC8; i += 256) *reinterpret_cast<u32x4*>(&sDY[i * 8]) = u32x4{0u, 0u, 0u, 0u};
+  for (int i = tid; i < (p.H + 2) * (p.W + 2) * 4; i += 256) *reinterpret_cast<u32x4*>(&sX[i * 8]) = u32x4{0u, 0u, 0u, 0u};
+  __syncthreads();
+  // XCD-aware: block b runs on XCD b % 8; the NCI slices of group gid share that XCD
+  const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
+  const int cig = j % NCI, gid = (j / NCI) * 8 + xcd;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  switch (wave) {
+    case 0: wgrad_body<CIN, 0, 7>(p, sDY, sX, gid, cig * 32); break;
+    case 1: wgrad_body<CIN, 7, 7>(p, sDY, sX, gid, cig * 32); break;
+    case 2: wgrad_body<CIN, 14, 7>(p, sDY, sX, gid, cig * 32); break;
+    default: wgrad_body<CIN, 21, 6>(p, sDY, sX, gid, cig * 32); break;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_reduce(const float* __restrict__ part, int G, int64_t n, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int g = 0; g < G; ++g) s += part[(int64_t)g * n + i];
+  out[i] = s;
+}
+
+// ------------------------------------------------------------------------------------
+struct Plan {
+  int grid_d, grid_w, G;
+  int64_t gn_part, w_part;
+};
+
+Plan make_plan(int n, int h, int w, int cin) {
+  Plan pl;
+  const int ncu = num_cus();
+  pl.grid_d = n < 2 * ncu ? n : 2 * ncu;
+  const int nci = cin == 96 ? 3 : 1;
+  int J = (2 * ncu) / (8 * nci);
+  if (J < 1) J = 1;
+  pl.G = 8 * J;
+  pl.grid_w = 8 * nci * J;
+  pl.gn_part = (int64_t)pl.grid_d * 3 * COUT;
+  pl.w_part = (int64_t)pl.G * 9 * COUT * cin;
+  (void)h;
+  (void)w;
+  return pl;
+}
+
+template <typename K>
+void set_lds_attr(K kernel) {
+  (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+template <int NPT, bool DGRAD, int NCH>
+void launch_bwd_data(const BwdDataParams& p, int grid, size_t lds, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    set_lds_attr(k_bwd_data<NPT, DGRAD, NCH>);
+    attr = true;
+  }
+  hipLaunchKernelGGL((k_bwd_data<NPT, DGRAD, NCH>), dim3(grid), dim3(256), lds, s, p);
+}
+
+template <bool DGRAD>
+int dispatch_bwd_data(const BwdDataParams& p, int grid, hipStream_t s) {
+  const int P = p.H * p.W;
+  const size_t lds = (size_t)bwd_data_lds(P);
+  if (lds > 160 * 1024) {
+    snprintf(g_err, sizeof g_err, "mc_conv_gn_bwd: board %dx%d needs %zu B LDS", p.H, p.W, lds);
+    return MS_EINVAL;
+  }
+  if (P <= 128) launch_bwd_data<1, DGRAD, 13>(p, grid, lds, s);
+  else if (P <= 256) launch_bwd_data<2, DGRAD, 13>(p, grid, lds, s);
+  else if (P <= 384) launch_bwd_data<3, DGRAD, 25>(p, grid, lds, s);
+  else if (P <= 512) launch_bwd_data<4, DGRAD, 25>(p, grid, lds, s);
+  else {
+    snprintf(g_err, sizeof g_err, "mc_conv_gn_bwd: %d pixels > 512 unsupported", P);
+    return MS_EINVAL;
+  }
+  return MS_OK;
+}
+
+template <int CIN>
+void launch_wgrad(const WgradParams& p, int grid, size_t lds, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    set_lds_attr(k_wgrad<CIN>);
+    attr = true;
+  }
+  hipLaunchKernelGGL((k_wgrad<CIN>), dim3(grid), dim3(256), lds, s, p);
+}
+
+int check_launch(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof g_err, "%s launch: %s", what, hipGetErrorString(e));
+    return MS_EHIP;
+  }
+  return MS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t mc_conv_gn_bwd_workspace(int32_t n, int32_t h, int32_t w_, int32_t cin) {
+  if (n <= 0 || h <= 0 || w_ <= 0 || (cin != 16 && cin != 96)) return -1;
+  const Plan pl = make_plan(n, h, w_, cin);
+  return pl.gn_part + pl.w_part;
+}
+
+int mc_conv_gn_bwd(const uint16_t* dout, const uint16_t* out, const uint16_t* ysave, const float* stats,
+                   const float* gamma, const float* dmask, const uint16_t* x, const uint16_t* wT,
+                   const uint16_t* addend, uint16_t* dy, uint16_t* dz, uint16_t* dx, float* dw, float* dgn,
+                   float* work, int64_t work_floats, int32_t n, int32_t h, int32_t w_, int32_t cin,
+                   void* stream) {
+  if (!dout || !out || !ysave || !stats || !gamma || !x || !dy || !dw || !dgn || !work || n <= 0 || h <= 0 ||
+      w_ <= 0) {
+    snprintf(g_err, sizeof g_err, "mc_conv_gn_bwd: bad argument");
+    return MS_EINVAL;
+  }
+  if (cin != 16 && cin != 96) {
+    snprintf(g_err, sizeof g_err, "mc_conv_gn_bwd: cin %d unsupported (16 or 96)", cin);
+    return MS_EINVAL;
+  }
+  if ((wT == nullptr) != (dx == nullptr) || (wT && cin != 96) || (addend && !wT)) {
+    snprintf(g_err, sizeof g_err, "mc_conv_gn_bwd: dx needs wT (and cin 96); addend needs dx");
+    return MS_EINVAL;
+  }
+  const Plan pl = make_plan(n, h, w_, cin);
+  if (work_floats < pl.gn_part + pl.w_part) {
+    snprintf(g_err, sizeof g_err, "mc_conv_gn_bwd: workspace %lld < %lld floats", (long long)work_floats,
+             (long long)(pl.gn_part + pl.w_part));
+    return MS_EINVAL;
+  }
+  if (wgrad_lds(h, w_) > 160 * 1024) {
+    snprintf(g_err, sizeof g_err, "mc_conv_gn_bwd: board %dx%d too large", h, w_);
+    return MS_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  BwdDataParams bp;
+  bp.dout = reinterpret_cast<const __bf16*>(dout);
+  bp.out = reinterpret_cast<const __bf16*>(out);
+  bp.y = reinterpret_cast<const __bf16*>(ysave);
+  bp.stats = stats;
+  bp.gamma = gamma;
+  bp.dmask = dmask;
+  bp.wT = reinterpret_cast<const __bf16*>(wT);
+  bp.addend = reinterpret_cast<const __bf16*>(addend);
+  bp.dy = reinterpret_cast<__bf16*>(dy);
+  bp.dz = reinterpret_cast<__bf16*>(dz);
+  bp.dx = reinterpret_cast<__bf16*>(dx);
+  bp.part = work;
+  bp.N = n;
+  bp.H = h;
+  bp.W = w_;
+  int rc = wT ? dispatch_bwd_data<true>(bp, pl.grid_d, s) : dispatch_bwd_data<false>(bp, pl.grid_d, s);
+  if (rc) return rc;
+  if ((rc = check_launch("k_bwd_data"))) return rc;
+  hipLaunchKernelGGL(k_reduce, dim3((3 * COUT + 255) / 256), dim3(256), 0, s, (const float*)work, pl.grid_d,
+                     (int64_t)3 * COUT, dgn);
+  if ((rc = check_launch("k_reduce"))) return rc;
+
+  WgradParams wp;
+  wp.dy = reinterpret_cast<const __bf16*>(dy);
+  wp.x = reinterpret_cast<const __bf16*>(x);
+  wp.part = work + pl.gn_part;
+  wp.N = n;
+  wp.H = h;
+  wp.W = w_;
+  wp.G = pl.G;
+  const size_t lds = (size_t)wgrad_lds(h, w_);
+  if (cin == 96) launch_wgrad<96>(wp, pl.grid_w, lds, s);
+  else launch_wgrad<16>(wp, pl.grid_w, lds, s);
+  if ((rc = check_launch("k_wgrad"))) return rc;
+  const int64_t nw = (int64_t)9 * COUT * cin;
+  hipLaunchKernelGGL(k_reduce, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, (const float*)(work + pl.gn_part),
+                     pl.G, nw, dw);
+  return check_launch("k_reduce");
+}
+
+}  // extern "C"

@@ -1,0 +1,56 @@
+// mscnn_common.h — types and wave helpers shared by the fused residual-CNN
+// kernels (mscnn.hip forward, mscnn_bwd.hip backward).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+namespace mc {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+// native vector: HIP's uint4 struct copies through memcpy and is left in scratch
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int COUT = 96;  // trunk width of the shipped configs (stem_channels)
+constexpr int NGRP = 6;   // GroupNorm groups (96 / 16)
+constexpr int WAVES = 4;  // 256-thread workgroups
+
+extern thread_local char g_err[256];
+
+int num_cus();
+
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, true));
+}
+
+// sum over each 16-lane row; the result is valid in lanes 15, 31, 47, 63
+__device__ __forceinline__ float row_sum16(float v) {
+  v += dppf<0x111>(v);
+  v += dppf<0x112>(v);
+  v += dppf<0x114>(v);
+  v += dppf<0x118>(v);
+  return v;
+}
+
+__device__ __forceinline__ float readlane_f(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+
+// ds_read_b64_tr_b16: per 16-lane group, lane 4q+p addresses row q / columns
+// 4p..4p+3 of a 4x16 block of 16-bit elements; lane i receives column i.
+__device__ __forceinline__ bf16x4 lds_tr4(const __bf16* p) {
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+  return __builtin_bit_cast(bf16x4, v);
+}
+
+__device__ __forceinline__ bf16x8 cat8(bf16x4 lo, bf16x4 hi) {
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+}  // namespace mc

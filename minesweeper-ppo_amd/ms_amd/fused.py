@@ -80,3 +80,56 @@ def conv_gn_fwd(x: torch.Tensor, wt: torch.Tensor, bias: torch.Tensor, gamma: to
     _check(_fwd(L.ptr(x), L.ptr(wt), L.ptr(b), L.ptr(g), L.ptr(be), L.ptr(res), L.ptr(dmask), L.ptr(out),
                 L.ptr(y), L.ptr(stats), n, H, W, cin, eps, L.stream_ptr(dev)))
     return out, y, stats
+
+
+_bwd = None
+_bwd_ws = None
+
+
+def prep_weight_t(w: torch.Tensor) -> torch.Tensor:
+    """[96, 96, 3, 3] nn.Conv2d weight -> bf16 [9, ci, co] (the dgrad operand W[tap]^T)."""
+    co, ci = w.shape[0], w.shape[1]
+    return w.detach().permute(2, 3, 1, 0).reshape(9, ci, co).to(torch.bfloat16).contiguous()
+
+
+def dw_to_conv(dw: torch.Tensor, cin_real: int) -> torch.Tensor:
+    """f32 [9, 96, cin] (tap, co, ci) -> nn.Conv2d weight layout [96, cin_real, 3, 3]."""
+    return dw.view(3, 3, COUT, dw.shape[-1]).permute(2, 3, 0, 1)[:, :cin_real].contiguous()
+
+
+def conv_gn_bwd(dout: torch.Tensor, out: torch.Tensor, y: torch.Tensor, stats: torch.Tensor, gamma: torch.Tensor,
+                x: torch.Tensor, H: int, W: int, wT: Optional[torch.Tensor] = None,
+                dmask: Optional[torch.Tensor] = None, addend: Optional[torch.Tensor] = None, want_dz: bool = False):
+    """Backward of conv_gn_fwd. Returns (dx | None, dz | None, dw f32 [9,96,cin], dgn f32 [3,96] =
+    d gamma, d beta, d bias). dx (bf16, NHWC) is produced iff the dgrad weights ``wT`` are given."""
+    global _bwd, _bwd_ws
+    if _bwd is None:
+        _bwd = _fn("mc_conv_gn_bwd", [_vp] * 15 + [ctypes.c_int64] + [_i32] * 4 + [_vp])
+        _bwd_ws = _fn("mc_conv_gn_bwd_workspace", [_i32] * 4)
+        _bwd_ws.restype = ctypes.c_int64
+    n, p, cin = x.shape
+    dev = x.device
+    for t in (dout, out, y):
+        assert t.shape == (n, p, COUT) and t.dtype == torch.bfloat16 and t.is_contiguous()
+    assert x.dtype == torch.bfloat16 and x.is_contiguous() and p == H * W
+    assert stats.shape == (n, NGROUPS, 2) and stats.dtype == torch.float32
+    if wT is not None:
+        assert wT.shape == (9, cin, COUT) and wT.dtype == torch.bfloat16 and wT.is_contiguous()
+    if addend is not None:
+        assert addend.shape == (n, p, cin) and addend.dtype == torch.bfloat16 and addend.is_contiguous()
+    if dmask is not None:
+        dmask = dmask.to(torch.float32).contiguous()
+    g = gamma.detach().to(torch.float32).contiguous()
+    dy = torch.empty((n, p, COUT), dtype=torch.bfloat16, device=dev)
+    dz = torch.empty_like(dy) if want_dz else None
+    dx = torch.empty((n, p, cin), dtype=torch.bfloat16, device=dev) if wT is not None else None
+    dw = torch.empty((9, COUT, cin), dtype=torch.float32, device=dev)
+    dgn = torch.empty((3, COUT), dtype=torch.float32, device=dev)
+    nws = int(_bwd_ws(n, H, W, cin))
+    if nws < 0:
+        raise L.MsEnvError("mc_conv_gn_bwd_workspace: bad sizes")
+    work = torch.empty(nws, dtype=torch.float32, device=dev)
+    _check(_bwd(L.ptr(dout), L.ptr(out), L.ptr(y), L.ptr(stats), L.ptr(g), L.ptr(dmask), L.ptr(x), L.ptr(wT),
+                L.ptr(addend), L.ptr(dy), L.ptr(dz), L.ptr(dx), L.ptr(dw), L.ptr(dgn), L.ptr(work), nws,
+                n, H, W, cin, L.stream_ptr(dev)))
+    return dx, dz, dw, dgn

@@ -19,6 +19,27 @@ from typing import Dict, Optional
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
+
+
+class GroupNorm(nn.GroupNorm):
+    """nn.GroupNorm with the affine step done as plain elementwise ops.
+
+    Same parameters / state_dict as nn.GroupNorm. On this image's PyTorch-ROCm
+    (2.10 + ROCm 7.0, gfx950) the fused GroupNorm backward returns wrong
+    weight/bias gradients once the batch reaches 256 samples (input gradients
+    stay right; tools/gn_torch_check.py), and PPO minibatches are
+    far above that. Normalising without affine and applying gamma/beta
+    elementwise keeps autograd on correct kernels."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if not x.is_cuda:  # CPU kernels are right: keep the reference's exact op
+            return super().forward(x)
+        y = F.group_norm(x, self.num_groups, None, None, self.eps)
+        if not self.affine:
+            return y
+        shape = (1, -1) + (1,) * (x.dim() - 2)
+        return y * self.weight.view(shape) + self.bias.view(shape)
 
 
 def _conv3(cin: int, cout: int) -> nn.Conv2d:
@@ -37,9 +58,9 @@ class _ResidualBlock(nn.Module):
     def __init__(self, channels: int, groups: int, dropout: float = 0.0) -> None:
         super().__init__()
         self.conv1 = _conv3(channels, channels)
-        self.norm1 = nn.GroupNorm(groups, channels)
+        self.norm1 = GroupNorm(groups, channels)
         self.conv2 = _conv3(channels, channels)
-        self.norm2 = nn.GroupNorm(groups, channels)
+        self.norm2 = GroupNorm(groups, channels)
         self.dropout = nn.Dropout2d(dropout) if dropout > 0 else nn.Identity()
         self.act = nn.ReLU(inplace=True)
 
@@ -62,7 +83,7 @@ class CNNResidualPolicy(nn.Module):
             raise ValueError("blocks must be positive")
         C = stem_channels
         groups = max(1, C // 16)
-        self.stem = nn.Sequential(_conv3(in_channels, C), nn.GroupNorm(groups, C), nn.ReLU(inplace=True))
+        self.stem = nn.Sequential(_conv3(in_channels, C), GroupNorm(groups, C), nn.ReLU(inplace=True))
         self.residual_stack = nn.Sequential(*(_ResidualBlock(C, groups, dropout) for _ in range(blocks)))
         self.policy_head = _pointwise_head(C)
         self.value_head = nn.Sequential(
@@ -104,8 +125,8 @@ class CNNPolicy(nn.Module):
             raise ValueError("hidden must be positive")
         feat = 64
         self.backbone = nn.Sequential(
-            _conv3(in_channels, 32), nn.ReLU(inplace=True), nn.GroupNorm(4, 32),
-            _conv3(32, 64), nn.ReLU(inplace=True), nn.GroupNorm(8, 64),
+            _conv3(in_channels, 32), nn.ReLU(inplace=True), GroupNorm(4, 32),
+            _conv3(32, 64), nn.ReLU(inplace=True), GroupNorm(8, 64),
             _conv3(64, feat), nn.ReLU(inplace=True),
         )
         self.policy_head = nn.Conv2d(feat, 1, kernel_size=1)

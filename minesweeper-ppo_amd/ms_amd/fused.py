@@ -133,3 +133,116 @@ def conv_gn_bwd(dout: torch.Tensor, out: torch.Tensor, y: torch.Tensor, stats: t
                 L.ptr(addend), L.ptr(dy), L.ptr(dz), L.ptr(dx), L.ptr(dw), L.ptr(dgn), L.ptr(work), nws,
                 n, H, W, cin, L.stream_ptr(dev)))
     return dx, dz, dw, dgn
+
+
+# ------------------------------------------------------------------------------------
+# Whole-trunk fast path for CNNResidualPolicy (cnn_residual.py:30-96): stem + residual
+# blocks as fused layers, activations NHWC bf16, autograd through mc_conv_gn_bwd.
+
+_wcache: dict = {}
+
+
+def _packed(w: torch.Tensor, kind: str, cin_pad: int = 0) -> torch.Tensor:
+    """bf16 re-layout of a conv weight, cached until the optimizer bumps its version."""
+    key = (id(w), kind)
+    hit = _wcache.get(key)
+    if hit is not None and hit[0] == w._version and hit[1] is w:
+        return hit[2]
+    t = prep_weight(w.detach(), cin_pad) if kind == "f" else prep_weight_t(w.detach())
+    _wcache[key] = (w._version, w, t)
+    return t
+
+
+def trunk_layers(model) -> list:
+    """[(conv, norm)] in execution order: stem, then (conv1, norm1), (conv2, norm2) per block."""
+    layers = [(model.stem[0], model.stem[1])]
+    for blk in model.residual_stack:
+        layers += [(blk.conv1, blk.norm1), (blk.conv2, blk.norm2)]
+    return layers
+
+
+def _trunk_forward(x0, layers, H, W, dmasks, save):
+    """Runs every layer; with ``save`` returns the tensors the backward needs:
+    acts[l] = input of layer l (acts[l + 1] = its output), ys[l], sts[l]."""
+    acts, ys, sts = [x0], [], []
+    x, blk_in = x0, None
+    for li, (conv, norm) in enumerate(layers):
+        wt = _packed(conv.weight, "f", x.shape[-1])
+        res = dm = None
+        if li % 2 == 1:  # first half of a block: Dropout2d after the ReLU
+            blk_in = x
+            dm = dmasks[(li - 1) // 2] if dmasks is not None else None
+        elif li > 0:  # second half: + the block input, then ReLU
+            res = blk_in
+        x, y, st = conv_gn_fwd(x, wt, conv.bias, norm.weight, norm.bias, H, W, res=res, dmask=dm, save=save,
+                               eps=norm.eps)
+        if save:
+            acts.append(x)
+            ys.append(y)
+            sts.append(st)
+    return x, acts, ys, sts
+
+
+class _TrunkFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x0, H, W, dmasks, layers, *params):
+        out, acts, ys, sts = _trunk_forward(x0, layers, H, W, dmasks, save=True)
+        ctx.H, ctx.W, ctx.layers, ctx.dmasks = H, W, layers, dmasks
+        ctx.saved = (acts, ys, sts)
+        ctx.nparams = len(params)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        acts, ys, sts = ctx.saved
+        layers, H, W, dmasks = ctx.layers, ctx.H, ctx.W, ctx.dmasks
+        grads = {}
+        d = dout.to(torch.bfloat16).contiguous()
+        nl = len(layers)
+        skip = None  # dz of a block's second half: the block input's skip gradient
+        for li in range(nl - 1, -1, -1):
+            conv, norm = layers[li]
+            x = acts[li]
+            cin_real = conv.weight.shape[1]
+            want_dx = li > 0
+            dm = dmasks[(li - 1) // 2] if (dmasks is not None and li % 2 == 1) else None
+            addend = skip if li % 2 == 1 else None
+            dx, dz, dw, dgn = conv_gn_bwd(d, acts[li + 1], ys[li], sts[li], norm.weight, x, H, W,
+                                          wT=_packed(conv.weight, "t") if want_dx else None, dmask=dm,
+                                          addend=addend, want_dz=(li % 2 == 0 and li > 0))
+            skip = dz
+            grads[id(conv.weight)] = dw_to_conv(dw, cin_real)
+            grads[id(conv.bias)] = dgn[2]
+            grads[id(norm.weight)] = dgn[0]
+            grads[id(norm.bias)] = dgn[1]
+            d = dx
+        ctx.saved = None
+        out = [None, None, None, None, None]
+        for conv, norm in layers:
+            for p in (conv.weight, conv.bias, norm.weight, norm.bias):
+                g = grads[id(p)]
+                out.append(g.to(p.dtype) if p.requires_grad else None)
+        return tuple(out)
+
+
+def trunk_params(layers) -> list:
+    return [p for conv, norm in layers for p in (conv.weight, conv.bias, norm.weight, norm.bias)]
+
+
+def fused_features(model, obs: torch.Tensor) -> torch.Tensor:
+    """Trunk features of CNNResidualPolicy as NHWC bf16 [N, H*W, 96] via the fused kernels.
+    Dropout2d masks are drawn here (torch RNG) when the model is in training mode."""
+    n, c, H, W = obs.shape
+    layers = trunk_layers(model)
+    x0 = obs_to_nhwc(obs, 16)
+    nblk = len(model.residual_stack)
+    p = model.residual_stack[0].dropout.p if isinstance(model.residual_stack[0].dropout, torch.nn.Dropout2d) else 0.0
+    dmasks = None
+    if model.training and p > 0:
+        keep = torch.rand(nblk, n, COUT, device=obs.device) >= p
+        dmasks = [(keep[i].float() * (1.0 / (1.0 - p))).contiguous() for i in range(nblk)]
+    params = trunk_params(layers)
+    if torch.is_grad_enabled() and any(q.requires_grad for q in params):
+        return _TrunkFn.apply(x0, H, W, dmasks, layers, *params)
+    out, _, _, _ = _trunk_forward(x0, layers, H, W, dmasks, save=False)
+    return out

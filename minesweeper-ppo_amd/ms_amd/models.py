@@ -15,6 +15,7 @@ activations to NHWC, which MIOpen's MFMA conv kernels prefer.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Optional
 
 import torch
@@ -94,13 +95,42 @@ class CNNResidualPolicy(nn.Module):
         )
         self.mine_head = _pointwise_head(C)
 
+        # fused MFMA trunk (csrc/mscnn*.hip) on HIP devices under bf16 autocast;
+        # MS_AMD_FUSED=0 forces the PyTorch op chain (A/B measurements)
+        self.fused = os.environ.get("MS_AMD_FUSED", "1") != "0"
+
     def set_gradient_checkpointing(self, enabled: bool) -> None:  # API parity (no-op, as the reference)
         return None
+
+    def use_fused(self, x: torch.Tensor) -> bool:
+        conv0 = self.stem[0]
+        return (self.fused and x.is_cuda and conv0.out_channels == 96 and conv0.in_channels <= 16
+                and x.shape[2] * x.shape[3] <= 512 and torch.is_autocast_enabled("cuda")
+                and torch.get_autocast_dtype("cuda") == torch.bfloat16)
 
     def features(self, x: torch.Tensor) -> torch.Tensor:
         return self.residual_stack(self.stem(x))
 
+    def _heads_nhwc(self, f: torch.Tensor, H: int, W: int, return_mine: bool):
+        """The three heads on NHWC trunk features [N, H*W, C]: a 1x1 conv is a linear map
+        over channels, so policy/mine heads are two GEMMs over N*H*W rows."""
+        def pointwise(head, t):
+            c0, c2 = head[0], head[2]
+            h = F.relu(F.linear(t, c0.weight.flatten(1), c0.bias))
+            return F.linear(h, c2.weight.flatten(1), c2.bias).squeeze(-1)
+        n = f.shape[0]
+        logits = pointwise(self.policy_head, f)  # [N, H*W], index r*W + c
+        vh = self.value_head
+        v = f.float().mean(1)  # AdaptiveAvgPool2d(1) + Flatten
+        value = vh[6](F.relu(vh[4](F.relu(vh[2](v))))).squeeze(-1)
+        if return_mine:
+            return logits, value, pointwise(self.mine_head, f.detach()).view(n, 1, H, W)
+        return logits, value
+
     def forward(self, x: torch.Tensor, return_mine: bool = False):
+        if self.use_fused(x):
+            from .fused import fused_features
+            return self._heads_nhwc(fused_features(self, x), x.shape[2], x.shape[3], return_mine)
         f = self.features(x)
         n = f.shape[0]
         # [N,1,H,W] -> [N,H*W], index r*W + c (cnn_residual.py:89)

@@ -53,6 +53,22 @@ int mc_conv_gn_bwd(const uint16_t* dout, const uint16_t* out, const uint16_t* ys
 /* f32 elements of scratch mc_conv_gn_bwd needs for these sizes. */
 int64_t mc_conv_gn_bwd_workspace(int32_t n, int32_t h, int32_t w_, int32_t cin);
 
+/* Policy + belief heads (cnn_residual.py:57-64, 85-96): per head
+ *   logit[m] = w2 . relu(W1 f[m] + b1) + b2      over rows m of f (bf16 [M][96], NHWC trunk features).
+ * w1: bf16 [nh*96][96] (policy rows first, then mine), b1/w2: f32 [nh*96], b2: f32 [nh].
+ * out_m == NULL computes the policy head only (nh = 1). Logits are f32 [M]. */
+int mc_heads_fwd(const uint16_t* f, const uint16_t* w1, const float* b1, const float* w2, const float* b2,
+                 float* out_p, float* out_m, int64_t M, void* stream);
+
+/* Backward of both heads. dlp/dlm: f32 [M] logit gradients (dlm may be NULL = 0).
+ * w1pT: bf16 [96][96] = policy W1 transposed. df (bf16 [M][96]) = policy-head input
+ * gradient (the mine head reads f.detach()) + gadd[m / P] (f32 [M/P][96], may be NULL).
+ * dw1: f32 [192][96], db1, dw2: f32 [192]. work: mc_heads_bwd_workspace(M) floats. */
+int mc_heads_bwd(const uint16_t* f, const float* dlp, const float* dlm, const uint16_t* w1, const uint16_t* w1pT,
+                 const float* b1, const float* w2, const float* gadd, int32_t P, uint16_t* df, float* dw1,
+                 float* db1, float* dw2, float* work, int64_t work_floats, int64_t M, void* stream);
+int64_t mc_heads_bwd_workspace(int64_t M);
+
 /* Thread-local message of the last failing mc_* call. */
 const char* mc_last_error(void);
 

@@ -49,6 +49,15 @@ __device__ __forceinline__ bf16x4 lds_tr4(const __bf16* p) {
   return __builtin_bit_cast(bf16x4, v);
 }
 
+// An SGPR zero the compiler cannot see through: indexing loop-invariant LDS data with
+// it keeps the loads inside a persistent loop instead of hoisting them all into
+// registers (which spills).
+__device__ __forceinline__ int opaque0() {
+  int z = 0;
+  asm volatile("" : "+s"(z));
+  return z;
+}
+
 __device__ __forceinline__ bf16x8 cat8(bf16x4 lo, bf16x4 hi) {
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }

@@ -1,0 +1,426 @@
+// msheads.hip — the policy and belief ("mine") heads of CNNResidualPolicy on MFMA.
+//
+// Reference (minesweeper/models/cnn_residual.py:57-64, 85-96): each head is
+//   Conv1x1(96, 96) -> ReLU -> Conv1x1(96, 1)
+// over the trunk features f; the policy head's output is the per-cell logit
+// (index r*W + c), the mine head runs on f.detach(). On NHWC features
+// f [M = N*H*W][96] a 1x1 conv is a GEMM over rows, so both heads together are
+// h = relu(f . W1^T + b1) (W1 = [policy W1; mine W1], 192 x 96), logit = h . w2 + b2.
+//
+// k_heads_fwd: per 128-row tile, H^T[c][px] on v_mfma_f32_32x32x16_bf16 (A = W1
+//   rows from LDS, B = f rows loaded straight from HBM), bias + ReLU + the w2 dot
+//   product in registers (the channel sum is in-lane plus one lane^32 add), one f32
+//   logit per row and head. f is read once for both heads; h never reaches HBM.
+// k_heads_bwd: per 128-row tile, recompute H[px][c] (A = f tile in LDS, B = W1),
+//   dh = dlogit * w2 * (h > 0) written to an LDS image (bf16), then
+//     df^T = W1p^T . dh_p^T  (policy only: the mine head sees f.detach()),
+//     dW1 += dh^T . f        (K = the tile's pixels; both operands K-major via
+//                             ds_read_b64_tr_b16 from the LDS images),
+//     dw2 += h^T . dlogit, db1 += sum dh  (in-lane accumulators);
+//   per-workgroup partials are summed by k_heads_reduce.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../../include/msenv.h"
+#include "../../include/mscnn.h"
+#include "mscnn_common.h"
+
+namespace {
+
+using namespace mc;
+
+constexpr int C = 96;        // trunk channels
+constexpr int NH = 192;      // both heads' hidden channels
+constexpr int WP = 104;      // padded weight row (elements): conflict-free ds_read_b128
+constexpr int TR = 128;      // rows per tile
+constexpr int PART = NH * C + 2 * NH;  // per-workgroup partial: dW1 | dw2 | db1
+
+struct HeadFwdParams {
+  const __bf16* f;
+  const __bf16* w1;  // [nh][96]
+  const float* b1;
+  const float* w2;
+  const float* b2;
+  float* out_p;
+  float* out_m;
+  int64_t M;
+};
+
+template <bool MINE>
+__global__ __launch_bounds__(256, 2) void k_heads_fwd(HeadFwdParams p) {
+  constexpr int NT = MINE ? 6 : 3;
+  __shared__ __attribute__((aligned(16))) __bf16 sW[NT * 32 * WP];
+  __shared__ __attribute__((aligned(16))) float sB1[NT * 32], sW2[NT * 32];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hh = lane >> 5;
+  for (int i = tid; i < NT * 32 * 12; i += 256) {
+    const int c = i / 12, k8 = i - c * 12;
+    *reinterpret_cast<u32x4*>(&sW[c * WP + k8 * 8]) = *reinterpret_cast<const u32x4*>(&p.w1[c * C + k8 * 8]);
+  }
+  for (int i = tid; i < NT * 32; i += 256) {
+    sB1[i] = p.b1[i];
+    sW2[i] = p.w2[i];
+  }
+  const float b2p = p.b2[0], b2m = MINE ? p.b2[1] : 0.f;
+  __syncthreads();
+  const int64_t ntiles = (p.M + TR - 1) / TR;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int zo = opaque0();
+    const int64_t row = tile * TR + wave * 32 + l32;
+    const bool valid = row < p.M;
+    bf16x8 b[6];
+#pragma unroll
+    for (int ks = 0; ks < 6; ++ks) {
+      u32x4 v = u32x4{0u, 0u, 0u, 0u};
+      if (valid) v = *reinterpret_cast<const u32x4*>(&p.f[row * C + ks * 16 + 8 * hh]);
+      b[ks] = __builtin_bit_cast(bf16x8, v);
+    }
+    f32x16 acc[NT];
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[ct][i] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 6; ++ks)
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sW[(ct * 32 + l32) * WP + ks * 16 + 8 * hh + zo]);
+        acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[ks], acc[ct], 0, 0, 0);
+      }
+    // acc[ct][r] = H^T[c = ct*32 + 8*(r>>2) + 4*hh + (r&3)][px = l32]
+    float s[2] = {0.f, 0.f};
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c0 = ct * 32 + 8 * g + 4 * hh;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s[ct / 3] += fmaxf(acc[ct][4 * g + j] + sB1[c0 + j + zo], 0.f) * sW2[c0 + j + zo];
+      }
+    s[0] += __shfl_xor(s[0], 32);
+    if (MINE) s[1] += __shfl_xor(s[1], 32);
+    if (valid && hh == 0) {
+      p.out_p[row] = s[0] + b2p;
+      if (MINE) p.out_m[row] = s[1] + b2m;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+struct HeadBwdParams {
+  const __bf16* f;
+  const float* dlp;
+  const float* dlm;
+  const __bf16* w1;   // [192][96]
+  const __bf16* w1pT; // [96 k][96 c] policy W1 transposed
+  const float* b1;
+  const float* w2;
+  const float* gadd;  // [M / P][96] or null: added to df (the value head's pooled gradient / P)
+  __bf16* df;
+  float* part;        // [gridDim][PART]
+  int64_t M;
+  int P;
+};
+
+// f tile [128][96]: 16-B chunk ch of row r at chunk ch ^ ((r >> 2) & 3)
+__device__ __forceinline__ int sf_off(int r, int col) {
+  return r * C + 8 * ((col >> 3) ^ ((r >> 2) & 3)) + (col & 7);
+}
+// dh image [128][192]: chunk ch of row r at ch ^ (((r >> 1) & 1) << 2 | (r >> 2) & 3)
+__device__ __forceinline__ int sd_off(int r, int col) {
+  return r * NH + 8 * ((col >> 3) ^ ((((r >> 1) & 1) << 2) | ((r >> 2) & 3))) + (col & 7);
+}
+
+struct HeadLds {
+  __bf16 w[NH * WP];     // W1 rows [c][k]
+  __bf16 wt[C * WP];     // policy W1^T rows [k][c]
+  __bf16 f[TR * C];      // swizzled f tile
+  __bf16 dh[TR * NH];    // swizzled dh image
+  float dl[2][TR];
+  float b1[NH], w2[NH];
+  float red[2][NH];
+};
+
+template <int T0, int NTW>
+__device__ __forceinline__ void heads_bwd_body(const HeadBwdParams& p, HeadLds& L) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hh = lane >> 5;
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  f32x16 dwacc[NTW];
+#pragma unroll
+  for (int t = 0; t < NTW; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dwacc[t][i] = 0.f;
+  float dw2acc[6], db1acc[6];
+#pragma unroll
+  for (int ct = 0; ct < 6; ++ct) dw2acc[ct] = db1acc[ct] = 0.f;
+
+  const int64_t ntiles = (p.M + TR - 1) / TR;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t base = tile * TR;
+    const int zo = opaque0();
+    // ---- stage f tile and the two logit gradients ----
+#pragma unroll
+    for (int i = 0; i < TR * 12 / 256; ++i) {
+      const int c = tid + 256 * i + zo, r = c / 12, ch = c - r * 12;
+      const int64_t row = base + r;
+      u32x4 v = u32x4{0u, 0u, 0u, 0u};
+      if (row < p.M) v = *reinterpret_cast<const u32x4*>(&p.f[row * C + ch * 8]);
+      *reinterpret_cast<u32x4*>(&L.f[sf_off(r, ch * 8)]) = v;
+    }
+    if (tid < TR) {
+      const int64_t row = base + tid;
+      L.dl[0][tid] = row < p.M ? p.dlp[row] : 0.f;
+      L.dl[1][tid] = (row < p.M && p.dlm) ? p.dlm[row] : 0.f;
+    }
+    __syncthreads();
+    // ---- recompute H[px][c] for this wave's 32 rows ----
+    {
+      f32x16 acc[6];
+#pragma unroll
+      for (int ct = 0; ct < 6; ++ct)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[ct][i] = 0.f;
+      const int ra = wave * 32 + l32 + zo;
+#pragma unroll
+      for (int ks = 0; ks < 6; ++ks) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&L.f[sf_off(ra, ks * 16 + 8 * hh)]);
+#pragma unroll
+        for (int ct = 0; ct < 6; ++ct) {
+          const bf16x8 b = *reinterpret_cast<const bf16x8*>(&L.w[(ct * 32 + l32) * WP + ks * 16 + 8 * hh + zo]);
+          acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[ct], 0, 0, 0);
+        }
+      }
+      // acc[ct][r] = H[px = wave*32 + 8*(r>>2) + 4*hh + (r&3)][c = ct*32 + l32]
+#pragma unroll
+      for (int ct = 0; ct < 6; ++ct) {
+        const int c = ct * 32 + l32;
+        const float b1c = L.b1[c + zo], w2c = L.w2[c + zo];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int pr = wave * 32 + 8 * (r >> 2) + 4 * hh + (r & 3) + zo;
+          const float dl = L.dl[ct / 3][pr];
+          const float hv = fmaxf(acc[ct][r] + b1c, 0.f);
+          dw2acc[ct] += hv * dl;
+          const float dh = hv > 0.f ? dl * w2c : 0.f;
+          db1acc[ct] += dh;
+          L.dh[sd_off(pr, c)] = (__bf16)dh;
+        }
+      }
+    }
+    __syncthreads();
+    // ---- df^T[k][px] = sum_c W1p^T[k][c] dh[px][c] (policy channels only) ----
+    {
+      f32x16 acc2[3];
+#pragma unroll
+      for (int kt = 0; kt < 3; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc2[kt][i] = 0.f;
+      const int rb = wave * 32 + l32 + zo;
+#pragma unroll
+      for (int ks = 0; ks < 6; ++ks) {
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(&L.dh[sd_off(rb, ks * 16 + 8 * hh)]);
+#pragma unroll
+        for (int kt = 0; kt < 3; ++kt) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(&L.wt[(kt * 32 + l32) * WP + ks * 16 + 8 * hh + zo]);
+          acc2[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc2[kt], 0, 0, 0);
+        }
+      }
+      // acc2[kt][r] = df[px = wave*32 + l32][k = kt*32 + 8*(r>>2) + 4*hh + (r&3)]
+      const int64_t row = base + rb;
+      if (row < p.M) {
+        const float* ga = p.gadd ? p.gadd + (row / p.P) * C : nullptr;
+#pragma unroll
+        for (int kt = 0; kt < 3; ++kt)
+#pragma unroll
+          for (int gg = 0; gg < 4; ++gg) {
+            const int k0 = kt * 32 + 8 * gg + 4 * hh;
+            float v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = acc2[kt][4 * gg + j];
+            if (ga) {
+              const float4 a4 = *reinterpret_cast<const float4*>(&ga[k0]);
+              v[0] += a4.x;
+              v[1] += a4.y;
+              v[2] += a4.z;
+              v[3] += a4.w;
+            }
+            const bf16x4 o = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+            *reinterpret_cast<bf16x4*>(&p.df[row * C + k0]) = o;
+          }
+      }
+    }
+    // ---- dW1[c][k] += sum_px dh[px][c] f[px][k] over the tile's 128 rows ----
+#pragma unroll 2
+    for (int kk = 0; kk < TR / 16; ++kk) {
+      const int r0 = kk * 16 + 8 * (g >> 1) + q + zo;
+      bf16x8 av[6], bv[3];
+#pragma unroll
+      for (int ct = T0 / 3; ct <= (T0 + NTW - 1) / 3; ++ct) {
+        const int col = ct * 32 + 16 * (g & 1) + 4 * pp;
+        av[ct] = cat8(lds_tr4(&L.dh[sd_off(r0, col)]), lds_tr4(&L.dh[sd_off(r0 + 4, col)]));
+      }
+#pragma unroll
+      for (int kt = 0; kt < 3; ++kt) {
+        const int col = kt * 32 + 16 * (g & 1) + 4 * pp;
+        bv[kt] = cat8(lds_tr4(&L.f[sf_off(r0, col)]), lds_tr4(&L.f[sf_off(r0 + 4, col)]));
+      }
+#pragma unroll
+      for (int t = 0; t < NTW; ++t) {
+        const int tt = T0 + t;
+        dwacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[tt / 3], bv[tt % 3], dwacc[t], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // f / dh images are re-staged by the next tile
+  }
+  // ---- partials ----
+  float* part = p.part + (size_t)blockIdx.x * PART;
+#pragma unroll
+  for (int t = 0; t < NTW; ++t) {
+    const int tt = T0 + t, ct = tt / 3, kt = tt % 3;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int c = ct * 32 + 8 * (r >> 2) + 4 * hh + (r & 3);
+      part[c * C + kt * 32 + l32] = dwacc[t][r];
+    }
+  }
+#pragma unroll
+  for (int ct = 0; ct < 6; ++ct) {
+    atomicAdd(&L.red[0][ct * 32 + l32], dw2acc[ct]);
+    atomicAdd(&L.red[1][ct * 32 + l32], db1acc[ct]);
+  }
+}
+
+__global__ __launch_bounds__(256, 1) void k_heads_bwd(HeadBwdParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  HeadLds& L = *reinterpret_cast<HeadLds*>(smem);
+  const int tid = threadIdx.x;
+  for (int i = tid; i < NH * 12; i += 256) {
+    const int c = i / 12, k8 = i - c * 12;
+    *reinterpret_cast<u32x4*>(&L.w[c * WP + k8 * 8]) = *reinterpret_cast<const u32x4*>(&p.w1[c * C + k8 * 8]);
+  }
+  for (int i = tid; i < C * 12; i += 256) {
+    const int k = i / 12, c8 = i - k * 12;
+    *reinterpret_cast<u32x4*>(&L.wt[k * WP + c8 * 8]) = *reinterpret_cast<const u32x4*>(&p.w1pT[k * C + c8 * 8]);
+  }
+  for (int i = tid; i < NH; i += 256) {
+    L.b1[i] = p.b1[i];
+    L.w2[i] = p.w2[i];
+    L.red[0][i] = L.red[1][i] = 0.f;
+  }
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  switch (wave) {  // 18 dW1 tiles (6 c-tiles x 3 k-tiles) split 5/5/4/4
+    case 0: heads_bwd_body<0, 5>(p, L); break;
+    case 1: heads_bwd_body<5, 5>(p, L); break;
+    case 2: heads_bwd_body<10, 4>(p, L); break;
+    default: heads_bwd_body<14, 4>(p, L); break;
+  }
+  __syncthreads();
+  float* part = p.part + (size_t)blockIdx.x * PART;
+  for (int i = tid; i < NH; i += 256) {
+    part[NH * C + i] = L.red[0][i];
+    part[NH * C + NH + i] = L.red[1][i];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_heads_reduce(const float* __restrict__ part, int G, float* __restrict__ dw1,
+                                                      float* __restrict__ dw2, float* __restrict__ db1) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= PART) return;
+  float s = 0.f;
+  for (int g = 0; g < G; ++g) s += part[(size_t)g * PART + i];
+  if (i < NH * C) dw1[i] = s;
+  else if (i < NH * C + NH) dw2[i - NH * C] = s;
+  else db1[i - NH * C - NH] = s;
+}
+
+int bwd_grid(int64_t M) {
+  const int64_t ntiles = (M + TR - 1) / TR;
+  const int ncu = num_cus();
+  return (int)(ntiles < ncu ? ntiles : ncu);
+}
+
+int check(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof g_err, "%s launch: %s", what, hipGetErrorString(e));
+    return MS_EHIP;
+  }
+  return MS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mc_heads_fwd(const uint16_t* f, const uint16_t* w1, const float* b1, const float* w2, const float* b2,
+                 float* out_p, float* out_m, int64_t M, void* stream) {
+  if (!f || !w1 || !b1 || !w2 || !b2 || !out_p || M <= 0) {
+    snprintf(g_err, sizeof g_err, "mc_heads_fwd: bad argument");
+    return MS_EINVAL;
+  }
+  HeadFwdParams p;
+  p.f = reinterpret_cast<const __bf16*>(f);
+  p.w1 = reinterpret_cast<const __bf16*>(w1);
+  p.b1 = b1;
+  p.w2 = w2;
+  p.b2 = b2;
+  p.out_p = out_p;
+  p.out_m = out_m;
+  p.M = M;
+  const int64_t ntiles = (M + TR - 1) / TR;
+  const int cap = 2 * num_cus();
+  const int grid = (int)(ntiles < cap ? ntiles : cap);
+  hipStream_t s = (hipStream_t)stream;
+  if (out_m) hipLaunchKernelGGL(k_heads_fwd<true>, dim3(grid), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(k_heads_fwd<false>, dim3(grid), dim3(256), 0, s, p);
+  return check("k_heads_fwd");
+}
+
+int64_t mc_heads_bwd_workspace(int64_t M) {
+  if (M <= 0) return -1;
+  return (int64_t)bwd_grid(M) * PART;
+}
+
+int mc_heads_bwd(const uint16_t* f, const float* dlp, const float* dlm, const uint16_t* w1, const uint16_t* w1pT,
+                 const float* b1, const float* w2, const float* gadd, int32_t P, uint16_t* df, float* dw1,
+                 float* db1, float* dw2, float* work, int64_t work_floats, int64_t M, void* stream) {
+  if (!f || !dlp || !w1 || !w1pT || !b1 || !w2 || !df || !dw1 || !db1 || !dw2 || !work || M <= 0 ||
+      (gadd && P <= 0)) {
+    snprintf(g_err, sizeof g_err, "mc_heads_bwd: bad argument");
+    return MS_EINVAL;
+  }
+  const int grid = bwd_grid(M);
+  if (work_floats < (int64_t)grid * PART) {
+    snprintf(g_err, sizeof g_err, "mc_heads_bwd: workspace too small");
+    return MS_EINVAL;
+  }
+  HeadBwdParams p;
+  p.f = reinterpret_cast<const __bf16*>(f);
+  p.dlp = dlp;
+  p.dlm = dlm;
+  p.w1 = reinterpret_cast<const __bf16*>(w1);
+  p.w1pT = reinterpret_cast<const __bf16*>(w1pT);
+  p.b1 = b1;
+  p.w2 = w2;
+  p.gadd = gadd;
+  p.df = reinterpret_cast<__bf16*>(df);
+  p.part = work;
+  p.M = M;
+  p.P = P;
+  hipStream_t s = (hipStream_t)stream;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_heads_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_heads_bwd, dim3(grid), dim3(256), sizeof(HeadLds), s, p);
+  int rc = check("k_heads_bwd");
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_heads_reduce, dim3((PART + 255) / 256), dim3(256), 0, s, (const float*)work, grid, dw1, dw2,
+                     db1);
+  return check("k_heads_reduce");
+}
+
+}  // extern "C"

@@ -246,3 +246,103 @@ def fused_features(model, obs: torch.Tensor) -> torch.Tensor:
         return _TrunkFn.apply(x0, H, W, dmasks, layers, *params)
     out, _, _, _ = _trunk_forward(x0, layers, H, W, dmasks, save=False)
     return out
+
+
+# ------------------------------------------------------------------------------------
+# Policy / belief heads + the value head's global average pool on NHWC features
+# (cnn_residual.py:57-96) through csrc/msheads.hip.
+
+_hf = _hb = _hbws = None
+_hcache: dict = {}
+
+
+def _head_pack(pol, mine):
+    """bf16 [192|96, 96] W1 (policy rows first), its policy transpose, f32 b1 / w2 / b2."""
+    heads = [pol] + ([mine] if mine is not None else [])
+    key = tuple((id(m.weight), m.weight._version, id(m.bias), m.bias._version) for h in heads for m in (h[0], h[2]))
+    hit = _hcache.get(len(heads))
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    w1 = torch.cat([h[0].weight.detach().reshape(COUT, COUT) for h in heads]).to(torch.bfloat16).contiguous()
+    w1pT = pol[0].weight.detach().reshape(COUT, COUT).t().to(torch.bfloat16).contiguous()
+    b1 = torch.cat([h[0].bias.detach() for h in heads]).float().contiguous()
+    w2 = torch.cat([h[2].weight.detach().reshape(COUT) for h in heads]).float().contiguous()
+    b2 = torch.cat([h[2].bias.detach().reshape(1) for h in heads]).float().contiguous()
+    packed = (w1, w1pT, b1, w2, b2)
+    _hcache[len(heads)] = (key, packed)
+    return packed
+
+
+def _heads_bind():
+    global _hf, _hb, _hbws
+    if _hf is None:
+        _hf = _fn("mc_heads_fwd", [_vp] * 7 + [ctypes.c_int64, _vp])
+        _hb = _fn("mc_heads_bwd", [_vp] * 8 + [_i32] + [_vp] * 5 + [ctypes.c_int64, ctypes.c_int64, _vp])
+        _hbws = _fn("mc_heads_bwd_workspace", [ctypes.c_int64])
+        _hbws.restype = ctypes.c_int64
+
+
+def heads_forward(f: torch.Tensor, pol, mine=None):
+    """f bf16 [N, P, 96] -> policy logits f32 [N, P] (and mine logits f32 [N, P] when ``mine``)."""
+    _heads_bind()
+    n, p, c = f.shape
+    assert c == COUT and f.dtype == torch.bfloat16 and f.is_contiguous()
+    w1, _, b1, w2, b2 = _head_pack(pol, mine)
+    lp = torch.empty((n, p), dtype=torch.float32, device=f.device)
+    lm = torch.empty_like(lp) if mine is not None else None
+    _check(_hf(L.ptr(f), L.ptr(w1), L.ptr(b1), L.ptr(w2), L.ptr(b2), L.ptr(lp), L.ptr(lm), n * p,
+               L.stream_ptr(f.device)))
+    return lp, lm
+
+
+class _HeadsFn(torch.autograd.Function):
+    """(f, head params) -> (policy logits, pooled features, mine logits). The mine head
+    reads f.detach() (cnn_residual.py:94), so its gradient never reaches f."""
+
+    @staticmethod
+    def forward(ctx, f, pol, mine, *params):
+        lp, lm = heads_forward(f, pol, mine)
+        pooled = f.float().mean(1)
+        ctx.save_for_backward(f)
+        ctx.pol, ctx.mine = pol, mine
+        return lp, pooled, lm
+
+    @staticmethod
+    def backward(ctx, dlp, dpool, dlm):
+        (f,) = ctx.saved_tensors
+        pol, mine = ctx.pol, ctx.mine
+        _heads_bind()
+        n, p, _ = f.shape
+        M = n * p
+        # the kernel always runs both heads' math; without a mine head its rows get dl = 0
+        w1, w1pT, b1, w2, _ = _head_pack(pol, mine if mine is not None else pol)
+        dev = f.device
+        dlp = dlp.float().contiguous() if dlp is not None else torch.zeros(n, p, device=dev)
+        dlm = dlm.float().contiguous() if (dlm is not None and mine is not None) else None
+        gadd = (dpool.float() / p).contiguous() if dpool is not None else None
+        df = torch.empty_like(f)
+        dw1 = torch.empty(2 * COUT, COUT, device=dev)
+        db1 = torch.empty(2 * COUT, device=dev)
+        dw2 = torch.empty(2 * COUT, device=dev)
+        nws = int(_hbws(M))
+        work = torch.empty(nws, device=dev)
+        _check(_hb(L.ptr(f), L.ptr(dlp), L.ptr(dlm), L.ptr(w1), L.ptr(w1pT), L.ptr(b1), L.ptr(w2), L.ptr(gadd), p,
+                   L.ptr(df), L.ptr(dw1), L.ptr(db1), L.ptr(dw2), L.ptr(work), nws, M, L.stream_ptr(dev)))
+        grads = [df, None, None]
+        for h, i, dl in [(pol, 0, dlp)] + ([(mine, 1, dlm)] if mine is not None else []):
+            sl = slice(i * COUT, (i + 1) * COUT)
+            db2 = dl.sum() if dl is not None else torch.zeros((), device=dev)
+            grads += [dw1[sl].reshape(h[0].weight.shape), db1[sl], dw2[sl].reshape(h[2].weight.shape),
+                      db2.reshape(h[2].bias.shape)]
+        return tuple(grads)
+
+
+def heads_apply(f: torch.Tensor, pol, mine=None):
+    """Policy logits f32 [N, P], pooled trunk features f32 [N, 96], mine logits [N, P] | None."""
+    params = []
+    for h in [pol] + ([mine] if mine is not None else []):
+        params += [h[0].weight, h[0].bias, h[2].weight, h[2].bias]
+    if torch.is_grad_enabled() and (f.requires_grad or any(q.requires_grad for q in params)):
+        return _HeadsFn.apply(f, pol, mine, *params)
+    lp, lm = heads_forward(f, pol, mine)
+    return lp, f.float().mean(1), lm

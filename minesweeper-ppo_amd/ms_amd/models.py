@@ -127,10 +127,21 @@ class CNNResidualPolicy(nn.Module):
             return logits, value, pointwise(self.mine_head, f.detach()).view(n, 1, H, W)
         return logits, value
 
+    def _heads_fused(self, f: torch.Tensor, H: int, W: int, return_mine: bool):
+        """Heads through csrc/msheads.hip: policy + mine logits and the pooled features in
+        one pass over f; the value MLP (N x 96 -> 1) stays a PyTorch op."""
+        from .fused import heads_apply
+        logits, pooled, mine = heads_apply(f, self.policy_head, self.mine_head if return_mine else None)
+        vh = self.value_head
+        value = vh[6](F.relu(vh[4](F.relu(vh[2](pooled))))).squeeze(-1)
+        if return_mine:
+            return logits, value, mine.view(f.shape[0], 1, H, W)
+        return logits, value
+
     def forward(self, x: torch.Tensor, return_mine: bool = False):
         if self.use_fused(x):
             from .fused import fused_features
-            return self._heads_nhwc(fused_features(self, x), x.shape[2], x.shape[3], return_mine)
+            return self._heads_fused(fused_features(self, x), x.shape[2], x.shape[3], return_mine)
         f = self.features(x)
         n = f.shape[0]
         # [N,1,H,W] -> [N,H*W], index r*W + c (cnn_residual.py:89)

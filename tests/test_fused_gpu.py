@@ -128,3 +128,45 @@ def test_conv_gn_bwd_matches_torch(gpu, H, W, cin, n, with_res):
     assert _rel(dgn[0], gr2.grad) < 6e-2
     if want_dx:
         assert _rel(dx, nhwc(xq.grad) + (add.float() if add is not None else 0)) < 6e-2
+
+
+@pytest.mark.parametrize("n,P", [(300, 256), (7, 81), (3, 30)])
+@pytest.mark.parametrize("with_mine", [True, False])
+def test_heads_match_torch(gpu, n, P, with_mine):
+    """Policy + mine heads (csrc/msheads.hip) and the pooled features vs a torch fp32
+    reference on the same bf16 features; gradients of f (policy path + pool only: the
+    mine head reads f.detach()) and of every head parameter. Relative L2 <= 1e-2."""
+    from ms_amd.fused import heads_apply
+    torch.manual_seed(3)
+    mk = lambda: torch.nn.Sequential(torch.nn.Conv2d(96, 96, 1), torch.nn.ReLU(),  # noqa: E731
+                                     torch.nn.Conv2d(96, 1, 1)).to(gpu)
+    pol, mine = mk(), mk()
+    f = (torch.randn(n, P, 96, device=gpu) * 0.7).to(torch.bfloat16).requires_grad_(True)
+    wl, wp, wm = torch.randn(n, P, device=gpu), torch.randn(n, 96, device=gpu), torch.randn(n, P, device=gpu)
+    lp, pooled, lm = heads_apply(f, pol, mine if with_mine else None)
+    loss = (lp * wl).sum() + (pooled * wp).sum() + ((lm * wm).sum() if with_mine else 0)
+    loss.backward()
+    got = {k: v.grad.clone() for k, v in list(pol.named_parameters()) + [("f", f)]}
+    got.update({"m" + k: v.grad.clone() for k, v in mine.named_parameters()} if with_mine else {})
+    for mod in (pol, mine):
+        mod.zero_grad(set_to_none=True)
+    fr = f.detach().float().requires_grad_(True)
+    # the kernel's W1 is bf16 (as under the reference's autocast): round it the same way
+    bfw = lambda w: w + (w.detach().to(torch.bfloat16).float() - w.detach())  # noqa: E731  (grad flows to w)
+    lin = lambda h, t: torch.nn.functional.linear(  # noqa: E731
+        torch.relu(torch.nn.functional.linear(t, bfw(h[0].weight.flatten(1)), h[0].bias)), h[2].weight.flatten(1),
+        h[2].bias).squeeze(-1)
+    rp = lin(pol, fr)
+    rpool = fr.mean(1)
+    rloss = (rp * wl).sum() + (rpool * wp).sum()
+    if with_mine:
+        rm = lin(mine, fr.detach())
+        rloss = rloss + (rm * wm).sum()
+    rloss.backward()
+    assert _rel(lp, rp) < 1e-2 and _rel(pooled, rpool) < 1e-3
+    if with_mine:
+        assert _rel(lm, rm) < 1e-2
+    ref = {k: v.grad for k, v in list(pol.named_parameters()) + [("f", fr)]}
+    ref.update({"m" + k: v.grad for k, v in mine.named_parameters()} if with_mine else {})
+    for k in ref:
+        assert _rel(got[k], ref[k]) < 1e-2, (k, _rel(got[k], ref[k]))

@@ -63,16 +63,18 @@ struct FwdParams {
 };
 
 // LDS layout (bf16 elements):
-//   region0: sX[(H+2)*(W+2)][CINP] zero-halo input tile; after the conv the
-//            same bytes hold sO[P][96] (y staged for the coalesced epilogue);
-//   sW[2][COUT][CINP]: double-buffered weights of one tap;
-//   f32 sRed[WAVES][NGRP], sGB[2][COUT] (gamma, beta).
+//   region0: sX[P+1][CINP] input tile, row P = zeros (every out-of-board tap read of
+//            every lane points there: no halo, no masking); after the conv the same
+//            bytes hold sO[P][96] (y staged for the coalesced epilogue);
+//   sW[COUT][CINP]: the weights of one tap (single buffer: ~75 KB in all, so two
+//            workgroups share a CU and cover one another's barriers and epilogues);
+//   f32 sRed[WAVES][NGRP], sGB[2][COUT] (gamma, beta), sAB[3][COUT].
 template <int CIN>
 constexpr int cinp() { return CIN + 8; }  // +16 B per pixel row: conflict-free ds_read_b128
 
 template <int CIN>
 __host__ __device__ inline int region0_elems(int H, int W) {
-  const int a = (H + 2) * (W + 2) * cinp<CIN>(), b = H * W * COUT;
+  const int a = (H * W + 1) * cinp<CIN>(), b = H * W * COUT;
   return ((a > b ? a : b) + 7) & ~7;
 }
 
@@ -106,18 +108,17 @@ __host__ __device__ inline int region0_elems(int H, int W) {
   } while (0)
 
 template <int CIN, int NPT, bool FULL>
-__global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
+__global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int CINP = cinp<CIN>();
   constexpr int C8 = CIN / 8;
   constexpr int NPF = (NPT * 128 * C8 + 255) / 256;  // 16-B input chunks per thread
   constexpr int NWC = (COUT * C8 + 255) / 256;        // 16-B weight chunks per thread and tap
-  const int H = p.H, W = p.W, P = H * W, WP = W + 2;
-  const int nhalo = (H + 2) * WP;
+  const int H = p.H, W = p.W, P = H * W;
   __bf16* sX = reinterpret_cast<__bf16*>(smem);
   __bf16* sO = sX;
   __bf16* sW = sX + region0_elems<CIN>(H, W);
-  float* sRed = reinterpret_cast<float*>(sW + 2 * COUT * CINP);
+  float* sRed = reinterpret_cast<float*>(sW + COUT * CINP);
   float* sGB = sRed + WAVES * NGRP;  // [gamma | beta]
   float* sAB = sGB + 2 * COUT;        // per sample: [scale | shift | dropout scale]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -127,45 +128,33 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
     sGB[i] = p.gamma[i];
     sGB[COUT + i] = p.beta[i];
   }
-  int aoff[NPT];
-  bool aval[NPT];
+  int qr[NPT], qc[NPT];  // this lane's output pixel of each 32-pixel tile
 #pragma unroll
   for (int t = 0; t < NPT; ++t) {
-    const int px = (wave * NPT + t) * 32 + l32;
-    aval[t] = px < P;
-    const int r = aval[t] ? px / W : 0, c = aval[t] ? px - r * W : 0;
-    aoff[t] = ((r + 1) * WP + (c + 1)) * CINP + 8 * hh;
+    const int q = (wave * NPT + t) * 32 + l32;
+    qr[t] = q < P ? q / W : -1000;  // a pixel past P reads the zero row at every tap
+    qc[t] = q < P ? q - qr[t] * W : -1000;
   }
-  u32x4 xin[NPF];
   u32x4 wr[NWC];
-  if ((int)blockIdx.x < p.N) MC_LOAD_IN(blockIdx.x, xin);
   for (int n = blockIdx.x; n < p.N; n += gridDim.x) {
-    // ---- stage input tile (zero halo re-written: the epilogue reuses the region) ----
-    for (int i = tid; i < nhalo - P; i += 256) {  // border cells
-      const int b = i;                             // enumerate border: top, bottom rows, then sides
-      int cell;
-      if (b < WP) cell = b;
-      else if (b < 2 * WP) cell = (H + 1) * WP + (b - WP);
-      else {
-        const int k = b - 2 * WP, r = 1 + (k >> 1);
-        cell = r * WP + ((k & 1) ? WP - 1 : 0);
-      }
-      uint4* d = reinterpret_cast<uint4*>(&sX[cell * CINP]);
-#pragma unroll
-      for (int c8 = 0; c8 < C8; ++c8) d[c8] = make_uint4(0u, 0u, 0u, 0u);
-    }
+    // loop-variant copy of tid: keeps the per-chunk address math inside the loop instead of
+    // hoisting a dozen 64-bit addresses out of it (they would be spilled)
+    const int tid = threadIdx.x + opaque0();
+    // ---- stage the input tile (the zero row is re-written: the epilogue reuses region0).
+    // No cross-sample register prefetch: the CU's other workgroup computes meanwhile. ----
+    u32x4 xin[NPF];
+    MC_LOAD_IN(n, xin);
+    for (int i = tid; i < C8; i += 256) *reinterpret_cast<u32x4*>(&sX[P * CINP + i * 8]) = u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
     for (int k = 0; k < NPF; ++k) {
       const int i = tid + 256 * k;
       if (i < P * C8) {
         const int px = i / C8, c8 = i - px * C8;
-        const int r = px / W, c = px - r * W;
-        *reinterpret_cast<u32x4*>(&sX[((r + 1) * WP + c + 1) * CINP + c8 * 8]) = xin[k];
+        *reinterpret_cast<u32x4*>(&sX[px * CINP + c8 * 8]) = xin[k];
       }
     }
     MC_LOAD_W(0, wr);
     MC_STORE_W(0, wr);
-    const int nn = n + gridDim.x;
     __syncthreads();
 
     f32x16 acc[NPT][3];
@@ -177,29 +166,33 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
         for (int i = 0; i < 16; ++i) acc[t][ct][i] = 0.f;
 
     for (int tap = 0; tap < 9; ++tap) {
-      // vmcnt retires loads in issue order: the next sample's (HBM) input prefetch is
-      // issued on the last tap so no weight-tap wait ever queues behind it
       if (tap + 1 < 9) MC_LOAD_W(tap + 1, wr);
-      else if (nn < p.N) MC_LOAD_IN(nn, xin);
-      const __bf16* sWt = sW + (tap & 1) * COUT * CINP;
       const int dr = tap / 3 - 1, dc = tap % 3 - 1;
-      const int tshift = (dr * WP + dc) * CINP;
+      int aoff[NPT];
+#pragma unroll
+      for (int t = 0; t < NPT; ++t) {
+        const int sr = qr[t] + dr, sc = qc[t] + dc;
+        const bool v = (unsigned)sr < (unsigned)H && (unsigned)sc < (unsigned)W;
+        aoff[t] = (v ? sr * W + sc : P) * CINP + 8 * hh;
+      }
 #pragma unroll
       for (int k0 = 0; k0 < CIN; k0 += 16) {
         bf16x8 b[3];
 #pragma unroll
         for (int ct = 0; ct < 3; ++ct)
-          b[ct] = *reinterpret_cast<const bf16x8*>(&sWt[(ct * 32 + l32) * CINP + k0 + 8 * hh]);
+          b[ct] = *reinterpret_cast<const bf16x8*>(&sW[(ct * 32 + l32) * CINP + k0 + 8 * hh]);
 #pragma unroll
         for (int t = 0; t < NPT; ++t) {
-          bf16x8 a = *reinterpret_cast<const bf16x8*>(&sX[aoff[t] + tshift + k0]);
-          if (!FULL && !aval[t]) a = bf16x8{};
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sX[aoff[t] + k0]);
 #pragma unroll
           for (int ct = 0; ct < 3; ++ct) acc[t][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[ct], acc[t][ct], 0, 0, 0);
         }
       }
-      if (tap + 1 < 9) MC_STORE_W((tap + 1) & 1, wr);  // that buffer was last read in tap-1
-      __syncthreads();
+      __syncthreads();  // sW (and after the last tap sX) fully read
+      if (tap + 1 < 9) {
+        MC_STORE_W(0, wr);
+        __syncthreads();
+      }
     }
 
     // ---------------- epilogue A: bias, GroupNorm statistics, y -> LDS ----------------
@@ -312,7 +305,7 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd(FwdParams p) {
 template <int CIN, int NPT, bool FULL>
 int launch_fwd(const FwdParams& p, hipStream_t s) {
   constexpr int CINP = cinp<CIN>();
-  const size_t lds = (size_t)region0_elems<CIN>(p.H, p.W) * 2 + (size_t)2 * COUT * CINP * 2 + WAVES * NGRP * 4 +
+  const size_t lds = (size_t)region0_elems<CIN>(p.H, p.W) * 2 + (size_t)COUT * CINP * 2 + WAVES * NGRP * 4 +
                      5 * COUT * 4;
   if (lds > 160 * 1024) {
     snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd: board %dx%d needs %zu B LDS", p.H, p.W, lds);
@@ -324,8 +317,9 @@ int launch_fwd(const FwdParams& p, hipStream_t s) {
                               160 * 1024);
     attr_set = true;
   }
-  const int ncu = num_cus();
-  const int grid = p.N < ncu ? p.N : ncu;
+  const int per_cu = lds <= 80 * 1024 ? 2 : 1;
+  const int cap = per_cu * num_cus();
+  const int grid = p.N < cap ? p.N : cap;
   hipLaunchKernelGGL((k_conv_gn_fwd<CIN, NPT, FULL>), dim3(grid), dim3(256), lds, s, p);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {

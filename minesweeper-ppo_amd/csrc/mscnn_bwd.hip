@@ -59,7 +59,7 @@ __host__ __device__ constexpr int red_bytes() {  // sRed [PG][3][96] f32, aliase
 __host__ __device__ inline int bwd_data_lds(int P) { return dtile_bytes(P) + red_bytes() + 6 * COUT * 4; }
 
 template <int NPT, bool DGRAD, int NCH>
-__global__ __launch_bounds__(256, 2) void k_bwd_data(BwdDataParams p) {
+__global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int H = p.H, W = p.W, P = H * W;
   __bf16* sD = reinterpret_cast<__bf16*>(smem);  // [P+1][DCP] (row P = 0); later [P][96] dx staging
@@ -68,9 +68,6 @@ __global__ __launch_bounds__(256, 2) void k_bwd_data(BwdDataParams p) {
   float* sCo = reinterpret_cast<float*>(smem + dtile_bytes(P) + red_bytes());  // [3][96]
   float* sTmp = sCo + 3 * COUT;                                                 // [2][96]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hh = lane >> 5;
-  const int pg = tid / NC8, c8 = tid - pg * NC8;
-  const bool gact = tid < PG * NC8;
-  const int grp = c8 >> 1;
   const float inv_cnt = 1.0f / (16.0f * (float)P);
   float acc_g = 0.f, acc_b = 0.f, acc_bias = 0.f;  // tid < 96: running sums for channel tid
 
@@ -84,6 +81,12 @@ __global__ __launch_bounds__(256, 2) void k_bwd_data(BwdDataParams p) {
   }
 
   for (int n = blockIdx.x; n < p.N; n += gridDim.x) {
+    // loop-variant thread coordinates: keep the per-chunk address math inside the loop
+    // (hoisted out of it, a few dozen 64-bit addresses would be spilled)
+    const int tid = threadIdx.x + opaque0();
+    const int pg = tid / NC8, c8 = tid - pg * NC8;
+    const bool gact = tid < PG * NC8;
+    const int grp = c8 >> 1;
     // ---------------- pass 1: dz and per-channel sums ----------------
     float dm[8];
 #pragma unroll

@@ -143,7 +143,11 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
     // ---- stage the input tile (the zero row is re-written: the epilogue reuses region0).
     // No cross-sample register prefetch: the CU's other workgroup computes meanwhile. ----
     u32x4 xin[NPF];
+#ifndef MC_EXP_NO_IN
     MC_LOAD_IN(n, xin);
+#else
+    for (int k = 0; k < NPF; ++k) xin[k] = u32x4{1u, 2u, 3u, (unsigned)n};
+#endif
     for (int i = tid; i < C8; i += 256) *reinterpret_cast<u32x4*>(&sX[P * CINP + i * 8]) = u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
     for (int k = 0; k < NPF; ++k) {
@@ -166,7 +170,9 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
         for (int i = 0; i < 16; ++i) acc[t][ct][i] = 0.f;
 
     for (int tap = 0; tap < 9; ++tap) {
+#ifndef MC_EXP_NO_WLOAD
       if (tap + 1 < 9) MC_LOAD_W(tap + 1, wr);
+#endif
       const int dr = tap / 3 - 1, dc = tap % 3 - 1;
       int aoff[NPT];
 #pragma unroll
@@ -175,6 +181,9 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
         const bool v = (unsigned)sr < (unsigned)H && (unsigned)sc < (unsigned)W;
         aoff[t] = (v ? sr * W + sc : P) * CINP + 8 * hh;
       }
+#ifdef MC_EXP_NO_MFMA
+      if (p.N < 0)
+#endif
 #pragma unroll
       for (int k0 = 0; k0 < CIN; k0 += 16) {
         bf16x8 b[3];
@@ -189,10 +198,12 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
         }
       }
       __syncthreads();  // sW (and after the last tap sX) fully read
+#ifndef MC_EXP_NO_WLOAD
       if (tap + 1 < 9) {
         MC_STORE_W(0, wr);
         __syncthreads();
       }
+#endif
     }
 
     // ---------------- epilogue A: bias, GroupNorm statistics, y -> LDS ----------------
@@ -201,7 +212,11 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
     for (int ct = 0; ct < 3; ++ct) biasv[ct] = p.bias[ct * 32 + l32];
     float gmean[NGRP], grstd[NGRP];
     const float inv_cnt = 1.0f / (16.0f * (float)P);
+#ifdef MC_EXP_NO_STATS
+    for (int pass = 0; pass < 0; ++pass) {
+#else
     for (int pass = 0; pass < 2; ++pass) {
+#endif
       float part[3];
 #pragma unroll
       for (int ct = 0; ct < 3; ++ct) {
@@ -280,15 +295,17 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
     __syncthreads();
 
     // ---------------- epilogue B: coalesced 16-B chunks of [px][co] ----------------
+#ifdef MC_EXP_NO_EPI
+    if (p.N < 0)
+#endif
     for (int c = tid; c < P * (COUT / 8); c += 256) {
-      const int px = c / (COUT / 8), c8 = c - px * (COUT / 8);
-      const int co0 = c8 * 8;
-      const size_t o = ((size_t)n * P + px) * COUT + co0;
-      const uint4 yv = *reinterpret_cast<const uint4*>(&sO[px * COUT + co0]);
-      if (p.ysave) *reinterpret_cast<uint4*>(&p.ysave[o]) = yv;
+      const int co0 = (c % (COUT / 8)) * 8;
+      const size_t o = (size_t)n * P * COUT + (size_t)c * 8;
+      const u32x4 yv = *reinterpret_cast<const u32x4*>(&sO[c * 8]);
+      if (p.ysave) *reinterpret_cast<u32x4*>(&p.ysave[o]) = yv;
       const bf16x8 y8 = __builtin_bit_cast(bf16x8, yv);
       bf16x8 r8 = bf16x8{};
-      if (p.res) r8 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(&p.res[o]));
+      if (p.res) r8 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(&p.res[o]));
       bf16x8 o8;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -296,7 +313,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
         const float z = fmaxf((float)y8[j] * sAB[co] + sAB[COUT + co] + (float)r8[j], 0.f);
         o8[j] = (__bf16)(z * sAB[2 * COUT + co]);
       }
-      *reinterpret_cast<uint4*>(&p.out[o]) = __builtin_bit_cast(uint4, o8);
+      *reinterpret_cast<u32x4*>(&p.out[o]) = __builtin_bit_cast(u32x4, o8);
     }
     __syncthreads();  // region0 is re-staged with the next input
   }

@@ -1,0 +1,63 @@
+"""On-device greedy evaluation (ms_amd/eval.py) vs the reference's eval.py.
+
+CPU: AUROC / ECE / Wilson helpers against tests/golden/eval_metrics.npz (reference
+outputs on random inputs; 1e-6: rare float32 score ties / float32 vs float64 means).
+GPU: evaluate_vec with tests/eval_model.DetModel (exact fp32 logits, no argmax
+ties) against the reference's evaluate_vec run on CPU with the same model
+(tests/golden/eval_vec_*.npz): win rate, CI, steps, progress and invalid rate must be
+identical; belief AUROC / ECE within 1e-6 (same cells, same probabilities; AUROC
+ranks ties by position where the reference's quicksort order is unspecified, so a
+looser 2e-3 applies to it)."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+import torch
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_auroc_ece_match_reference():
+    from ms_amd.eval import compute_auroc, compute_ece
+    z = np.load(os.path.join(GOLDEN, "eval_metrics.npz"))
+    for i in range(3):
+        lab, sc = torch.from_numpy(z[f"labels{i}"]), torch.from_numpy(z[f"scores{i}"])
+        # float32 scores tie occasionally at n=20000; tie order is unspecified in the reference
+        assert compute_auroc(lab, sc) == pytest.approx(float(z[f"auroc{i}"]), abs=1e-6)
+        # the reference averages in float32 (numpy pairwise sums), this in float64
+        assert compute_ece(sc, lab) == pytest.approx(float(z[f"ece{i}"]), abs=1e-6)
+
+
+def test_auroc_ece_edge_cases():
+    from ms_amd.eval import compute_auroc, compute_ece
+    assert np.isnan(compute_auroc(torch.zeros(5), torch.rand(5)))
+    assert np.isnan(compute_ece(torch.zeros(0), torch.zeros(0)))
+    # p = 1.0 falls in the closed last bin
+    assert compute_ece(torch.tensor([1.0, 0.0]), torch.tensor([1.0, 0.0])) == pytest.approx(0.0)
+
+
+def test_wilson_interval():
+    from ms_amd.eval import wilson_interval
+    lo, hi = wilson_interval(872, 1000)
+    assert 0.84 < lo < 0.872 < hi < 0.90
+    assert all(np.isnan(v) for v in wilson_interval(0, 0))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("board", ["8x8x4", "9x9x10", "16x16x40"])
+def test_evaluate_vec_matches_reference(gpu, board):
+    from eval_model import DetModel
+    from ms_amd import EnvConfig
+    from ms_amd.eval import evaluate_vec
+    H, W, K = (int(v) for v in board.split("x"))
+    z = np.load(os.path.join(GOLDEN, f"eval_vec_{board}.npz"))
+    ref = dict(zip([str(k) for k in z["keys"]], z["values"]))
+    got = evaluate_vec(DetModel().to(gpu), EnvConfig(H=H, W=W, mine_count=K), episodes=int(z["episodes"]),
+                       seed=0, num_envs=int(z["num_envs"]))
+    for k in ("win_rate", "win_ci_low", "win_ci_high", "avg_steps", "avg_progress", "invalid_rate", "wins",
+              "episodes"):
+        assert got[k] == pytest.approx(ref[k], abs=1e-12), k
+    assert got["belief_ece"] == pytest.approx(ref["belief_ece"], abs=1e-6)
+    assert got["belief_auroc"] == pytest.approx(ref["belief_auroc"], abs=2e-3)

@@ -15,6 +15,7 @@ seed list, so the trajectories do not depend on the world size.
 from __future__ import annotations
 
 import argparse
+import math
 import csv
 import json
 import logging
@@ -23,6 +24,7 @@ import time
 from dataclasses import asdict, dataclass
 from typing import Dict
 
+import numpy as np
 import torch
 import yaml
 from torch.optim import AdamW
@@ -216,6 +218,37 @@ class Trainer:
         broadcast_module(self.model, self.info)
 
 
+def quick_eval_score(metrics: Dict[str, float]) -> float:
+    """train_rl.py:434-455: win rate plus small guess / AUROC bonuses (keys this build does
+    not compute are NaN and contribute nothing, as in the reference)."""
+    def _f(v):
+        try:
+            return float(v)
+        except (TypeError, ValueError):
+            return float("nan")
+    score = _f(metrics.get("win_rate"))
+    ge, gs, au = _f(metrics.get("guesses_per_episode")), _f(metrics.get("guess_success_rate")), \
+        _f(metrics.get("belief_auroc"))
+    if math.isfinite(ge):
+        score -= max(0.0, ge - 1.5) * 0.01
+        score += max(0.0, 1.5 - ge) * 0.005
+    if math.isfinite(gs):
+        score += max(0.0, gs - 0.75) * 0.05
+    if math.isfinite(au):
+        score += max(0.0, au - 0.93) * 0.02
+    return score
+
+
+def evaluate_model(model, env_cfg, *, episodes: int, num_envs: int, seed: int, pairs: int = 1,
+                   amp_dtype=None) -> Dict[str, float]:
+    """train_rl.py:49-69: ``pairs`` evaluations with seeds seed, seed+1, ... averaged."""
+    from .eval import evaluate_vec
+    runs = [evaluate_vec(model, env_cfg, episodes=episodes, seed=seed + i, num_envs=num_envs, amp_dtype=amp_dtype)
+            for i in range(max(1, pairs))]
+    keys = runs[0].keys()
+    return {k: float(np.mean([r[k] for r in runs])) for k in keys}
+
+
 def main(argv=None) -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=str, default=None)
@@ -226,10 +259,15 @@ def main(argv=None) -> None:
     ap.add_argument("--init_ckpt", type=str, default=None)
     ap.add_argument("--save_every", type=int, default=50)
     ap.add_argument("--amp", choices=["bf16", "fp16", "fp32"], default="bf16")
-    # accepted for CLI parity with train_rl.py:293-315 (evaluation is SURVEY.md §8f "next")
-    for flag in ("--eval_episodes", "--eval_num_envs", "--eval_quick_episodes", "--quick_eval_pairs",
-                 "--quick_eval_interval", "--eval_pairs"):
-        ap.add_argument(flag, type=int, default=None)
+    # evaluation flags of train_rl.py:297-305 (on-device greedy eval, ms_amd/eval.py)
+    ap.add_argument("--eval_episodes", type=int, default=2048)
+    ap.add_argument("--eval_num_envs", type=int, default=64)
+    ap.add_argument("--eval_quick_episodes", type=int, default=512)
+    ap.add_argument("--quick_eval_pairs", type=int, default=2)
+    ap.add_argument("--quick_eval_interval", type=int, default=10)
+    ap.add_argument("--eval_pairs", type=int, default=1)
+    ap.add_argument("--eval_amp", choices=["fp32", "bf16"], default="fp32",
+                    help="evaluation precision (the reference evaluates in fp32)")
     ap.add_argument("--skip_final_eval", action="store_true")
     ap.add_argument("--grad_checkpoint", action="store_true")
     ap.add_argument("--flash_attention", choices=["auto", "on", "off"], default="auto")
@@ -239,6 +277,9 @@ def main(argv=None) -> None:
     cfg, env_d, model_d, extras = load_config(args.config)
     if args.updates is not None:
         cfg.total_updates = int(args.updates)
+    training = extras.get("training", {}) if isinstance(extras, dict) else {}
+    patience = training.get("early_stop_patience")
+    patience = int(patience) if patience is not None else None
     logging.basicConfig(level=logging.INFO if info.is_main else logging.WARNING,
                         format="[%(asctime)s] %(message)s", datefmt="%H:%M:%S")
     log = logging.getLogger("ms_amd.train")
@@ -246,6 +287,8 @@ def main(argv=None) -> None:
     torch.cuda.set_device(device)
     tr = Trainer(cfg, env_d, model_d, extras, seed=args.seed, model_name=args.model, info=info, amp=args.amp,
                  device=device)
+    env_cfg = tr.vec.cfg
+    eval_amp = torch.bfloat16 if args.eval_amp == "bf16" else None
     if args.init_ckpt:
         tr.load_init(args.init_ckpt)
     if info.is_main:
@@ -254,12 +297,19 @@ def main(argv=None) -> None:
         log.info(f"Model: {tr.model_name} | params={n_params / 1e6:.2f}M | world={info.world} | "
                  f"envs/rank={tr.vec.num_envs}")
     rows = []
+    best_score, best_metrics, best_update, best_ckpt = float("-inf"), None, -1, None
+    stopped_early = False
+    quick_eps = max(0, min(args.eval_quick_episodes, args.eval_episodes))
     for update in range(cfg.total_updates):
         t0 = time.time()
         st = tr.update(update)
         dt = time.time() - t0
         row = {"update": update + 1, "seconds": dt, "steps": cfg.num_envs * cfg.steps_per_env, **st}
+        for k in ("quick_win_rate", "quick_guesses_per_ep", "quick_guess_success", "quick_belief_auroc",
+                  "quick_belief_ece", "quick_forced_guess_rate", "quick_safe_option_pick_rate", "quick_score"):
+            row[k] = None
         rows.append(row)
+        stop = False
         if info.is_main:
             extra = "".join(f" {k}={st[k]:.4f}" for k in ("aux_bce", "aux_calib") if k in st)
             log.info(f"upd {update + 1}/{cfg.total_updates} | {dt:.2f}s | steps={row['steps']} | "
@@ -267,6 +317,32 @@ def main(argv=None) -> None:
                      f"ent={st.get('entropy', float('nan')):.4f}{extra} ent_coef={st['ent_coef']:.4f}")
             if (update + 1) % max(1, args.save_every) == 0:
                 tr.checkpoint(os.path.join(args.out, "ckpt_latest.pt"))
+            if quick_eps > 0 and args.quick_eval_interval > 0 and (update + 1) % args.quick_eval_interval == 0:
+                mq = evaluate_model(tr.model, env_cfg, episodes=quick_eps,
+                                    seed=args.seed * 1000 + (update + 1) * 7,
+                                    num_envs=min(args.eval_num_envs, max(1, quick_eps // 8)),
+                                    pairs=args.quick_eval_pairs, amp_dtype=eval_amp)
+                score = quick_eval_score(mq)
+                row.update(quick_win_rate=mq["win_rate"], quick_belief_auroc=mq["belief_auroc"],
+                           quick_belief_ece=mq["belief_ece"], quick_forced_guess_rate=mq["forced_guess_rate"],
+                           quick_safe_option_pick_rate=mq["safe_option_pick_rate"], quick_score=score)
+                log.info("quick eval upd %d: win_rate=%.3f avg_steps=%.2f auroc=%.3f score=%.3f", update + 1,
+                         mq["win_rate"], mq["avg_steps"], mq["belief_auroc"], score)
+                if score > best_score or best_update < 0:
+                    best_score, best_metrics, best_update = score, mq, update + 1
+                    best_ckpt = os.path.join(args.out, "ckpt_best.pt")
+                    tr.checkpoint(best_ckpt, metric=mq)
+                if patience is not None and best_update >= 0 and (update + 1) - best_update >= patience:
+                    log.info("Early stopping at update %d (best score %.3f at update %d, patience=%d)",
+                             update + 1, best_score, best_update, patience)
+                    stop = True
+        if info.world > 1:  # every rank leaves the loop together
+            flag = torch.tensor([1.0 if stop else 0.0], device=device)
+            torch.distributed.all_reduce(flag, group=info.group)
+            stop = bool(flag.item() > 0)
+        if stop:
+            stopped_early = True
+            break
     if info.is_main:
         keys = sorted(set().union(*rows)) if rows else []
         with open(os.path.join(args.out, "train_metrics.csv"), "w", newline="") as f:
@@ -274,10 +350,29 @@ def main(argv=None) -> None:
             w.writeheader()
             for r in rows:
                 w.writerow(r)
-        tr.checkpoint(os.path.join(args.out, "ckpt_final.pt"))
+        final = os.path.join(args.out, "ckpt_final.pt")
+        tr.checkpoint(final)
+        last = final
+        if best_ckpt and os.path.exists(best_ckpt):  # evaluate the best weights (train_rl.py:703-718)
+            state = torch.load(best_ckpt, map_location=device, weights_only=True)
+            tr.model.load_state_dict(strip_compile_prefix(state["model"]), strict=False)
+            last = best_ckpt
+        metrics_raw = None
+        if not args.skip_final_eval and args.eval_episodes > 0 and args.eval_num_envs > 0:
+            eps = max(1, args.eval_episodes)
+            metrics_raw = evaluate_model(tr.model, env_cfg, episodes=eps, seed=args.seed * 17,
+                                         num_envs=min(args.eval_num_envs, eps), pairs=args.eval_pairs,
+                                         amp_dtype=eval_amp)
+            log.info("final eval: %s", {k: round(v, 4) for k, v in metrics_raw.items() if math.isfinite(v)})
         with open(os.path.join(args.out, "summary.json"), "w") as f:
-            json.dump({"checkpoint": "ckpt_final.pt", "metrics_raw": None, "model": tr.model_meta,
-                       "seed": args.seed, "world_size": info.world}, f)
+            json.dump({"checkpoint": os.path.basename(last), "metrics_raw": metrics_raw, "model": tr.model_meta,
+                       "seed": args.seed, "quick_eval_pairs": args.quick_eval_pairs,
+                       "quick_eval_interval": args.quick_eval_interval, "eval_pairs": args.eval_pairs,
+                       "best_quick_metrics": best_metrics,
+                       "best_quick_score": best_score if math.isfinite(best_score) else None,
+                       "best_checkpoint": os.path.basename(best_ckpt) if best_ckpt else None,
+                       "best_update": best_update, "stopped_early": stopped_early,
+                       "early_stop_patience": patience, "world_size": info.world}, f)
     if info.world > 1:
         torch.distributed.destroy_process_group()
 

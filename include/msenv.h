@@ -118,6 +118,21 @@ int ms_snapshot(ms_handle* h, uint8_t* mine, uint8_t* revealed, uint8_t* counts,
  * inc_lo, has_uint32, uinteger} (numpy's bit_generator.state layout). */
 int ms_rng_state(ms_handle* h, uint64_t* out, void* stream);
 
+/* Late-start resets (VecMinesweeper late_start_cfg, env.py:397-403, 416-466):
+ * from now on every reset (ms_reset: all envs; ms_step: the auto-reset of each
+ * done env) applies _apply_late_start with ONE generator shared by the envs of
+ * this handle, seeded like numpy default_rng(late_seed), consumed in env order.
+ * Arguments as the reference's cfg keys (prob, min_hidden, max_hidden,
+ * max_attempts, max_extra_steps; pass H*W for the default max_extra_steps), with
+ * the reference's clamps. Bit-exact with the reference for an unsharded handle
+ * (env_begin 0, env_count n_total); a shard gets its own stream. ms_step then
+ * requires its `done` output. */
+int ms_set_late_start(ms_handle* h, double prob, int32_t min_hidden, int32_t max_hidden,
+                      int32_t max_attempts, int32_t max_extra_steps, uint64_t late_seed);
+
+/* The late-start generator's state as u64[6] (ms_rng_state layout); synchronous. */
+int ms_late_rng_state(ms_handle* h, uint64_t* out);
+
 /* Synthetic policy: for global env g and step t,
  * x = splitmix64(0xC0FFEE ^ (g << 32) ^ t); MS_TAPE_UNIFORM picks the
  * (x mod popcount(mask))-th valid cell; MS_TAPE_SAFE_BIASED picks a non-mine

@@ -633,6 +633,73 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
 #define STAMP(k) do { } while (0)
 #endif
 
+// ---------------------------------------------------------------------------
+// One reveal on one board (MinesweeperEnv.step env.py:103-137 minus the reward /
+// step bookkeeping): first-click placement, mine hit, flood fill, win check.
+// Wave-uniform results: done, outcome, newly revealed, total revealed.
+// ---------------------------------------------------------------------------
+template <int H_, int W_>
+__device__ __forceinline__ void board_click(Pcg& rng, uint64_t& mine, uint64_t& rev, bool& fc, int cell,
+                                            const KParams& p, const uint64_t (&J)[4], uint32_t* sTab,
+                                            uint64_t* sR, const Geo<H_, W_>& g, int lane, bool& done,
+                                            int& outcome, uint32_t& newly, uint32_t& total_rev,
+                                            bool& mines_changed) {
+  const int H = g.H, W = g.W, A = g.A();
+  const uint64_t rowmask = g.rowmask();
+  const int ar = cell / W, ac = cell - (cell / W) * W;
+  done = false;
+  outcome = MS_OUTCOME_NONE;
+  newly = 0;
+  const bool cell_rev = (readlane64(rev, ar) >> ac) & 1ull;
+  if (!cell_rev) {
+    if (!fc) {
+      const Forbid F = make_forbid(cell, ar, ac, p.K, p.guarantee != 0, g);
+      bool ok = false;
+      if (!(p.dbg_flags & MS_DBG_FORCE_SERIAL_PLACEMENT)) {
+        if (p.K >= 1 && p.K <= 128 && !(p.dbg_flags & MS_DBG_FORCE_CHAIN_PLACEMENT))
+          ok = place_fixpoint(rng, mine, F, p.K, J, sTab, sR, g, lane);
+        else
+          ok = place_parallel(rng, mine, F, p.K, J, g, lane);
+      }
+      if (!ok) place_serial(rng, mine, F, p.K, g, lane);
+      fc = true;
+      mines_changed = true;
+    }
+    const bool hit = (readlane64(mine, ar) >> ac) & 1ull;
+    if (hit) {
+      if (lane == ar) rev |= 1ull << ac;
+      done = true;
+      outcome = MS_OUTCOME_LOSS;
+    } else {
+      // ---- flood_fill_reveal (env_numba.py:17-77) as dilation to fixpoint ----
+      const uint64_t U = wave_shr1(mine) | wave_shl1(mine);
+      const uint64_t nb = U | (U << 1) | (U >> 1) | (mine << 1) | (mine >> 1);
+      const uint64_t zero = ~nb & rowmask;
+      const uint64_t allow = ~mine & ~rev & (lane < H ? rowmask : 0ull);
+      uint64_t Fr = (lane == ar) ? (1ull << ac) : 0ull;
+      while (true) {
+        const uint64_t S = Fr & zero;
+        const uint64_t Dh = S | (S << 1) | (S >> 1);
+        const uint64_t Dv = Dh | wave_shr1(Dh) | wave_shl1(Dh);
+        const uint64_t Fn = Fr | (Dv & allow);
+        const bool changed = __ballot(Fn != Fr) != 0ull;
+        Fr = Fn;
+        if (!changed) break;
+      }
+      rev |= Fr;
+      newly = (uint32_t)__popcll(Fr);
+    }
+  }
+  // one reduction for both counts: total revealed (hi 16) | newly revealed (lo 16)
+  const uint32_t packed = wave_sum(((uint32_t)__popcll(rev) << 16) | newly);
+  total_rev = packed >> 16;
+  newly = packed & 0xffffu;
+  if (!cell_rev && outcome != MS_OUTCOME_LOSS && (int)total_rev >= A - p.K) {
+    done = true;
+    outcome = MS_OUTCOME_WIN;
+  }
+}
+
 template <int H_, int W_>
 __global__ __launch_bounds__(64) void k_step(KParams p) {
   __shared__ uint64_t sR[kWave];
@@ -643,8 +710,7 @@ __global__ __launch_bounds__(64) void k_step(KParams p) {
   if (env >= p.n) return;
   STAMP(0);
   const Geo<H_, W_> g(p.H, p.W);
-  const int H = g.H, W = g.W, A = g.A(), NW = g.NW();
-  const uint64_t rowmask = g.rowmask();
+  const int A = g.A(), NW = g.NW();
 
   EnvMeta* mp = p.meta + env;
   uint64_t* mwords = p.mine_words + env * NW;
@@ -678,67 +744,17 @@ __global__ __launch_bounds__(64) void k_step(KParams p) {
   int64_t cell64 = a % A;  // Python modulo (env.py:106)
   if (cell64 < 0) cell64 += A;
   const int cell = (int)cell64;
-  const int ar = cell / W, ac = cell - (cell / W) * W;
   STAMP(1);
 
   double reward = 0.0;
   bool done = false;
   int outcome = MS_OUTCOME_NONE;
-  uint32_t newly = 0;
+  uint32_t newly = 0, total_rev = 0;
   bool mines_changed = false;
-
-  const bool cell_rev = (readlane64(rev, ar) >> ac) & 1ull;
-  if (!cell_rev) {
-    if (!fc) {
-      const Forbid F = make_forbid(cell, ar, ac, p.K, p.guarantee != 0, g);
-      bool ok = false;
-      if (!(p.dbg_flags & MS_DBG_FORCE_SERIAL_PLACEMENT)) {
-        if (p.K >= 1 && p.K <= 128 && !(p.dbg_flags & MS_DBG_FORCE_CHAIN_PLACEMENT))
-          ok = place_fixpoint(rng, mine, F, p.K, J, sTab, sR, g, lane);
-        else
-          ok = place_parallel(rng, mine, F, p.K, J, g, lane);
-      }
-      if (!ok) place_serial(rng, mine, F, p.K, g, lane);
-      fc = true;
-      mines_changed = true;
-    }
-    STAMP(2);
-    const bool hit = (readlane64(mine, ar) >> ac) & 1ull;
-    if (hit) {
-      if (lane == ar) rev |= 1ull << ac;
-      done = true;
-      outcome = MS_OUTCOME_LOSS;
-      reward += p.loss_reward;
-    } else {
-      // ---- flood_fill_reveal (env_numba.py:17-77) as dilation to fixpoint ----
-      const uint64_t U = wave_shr1(mine) | wave_shl1(mine);
-      const uint64_t nb = U | (U << 1) | (U >> 1) | (mine << 1) | (mine >> 1);
-      const uint64_t zero = ~nb & rowmask;
-      const uint64_t allow = ~mine & ~rev & (lane < H ? rowmask : 0ull);
-      uint64_t Fr = (lane == ar) ? (1ull << ac) : 0ull;
-      while (true) {
-        const uint64_t S = Fr & zero;
-        const uint64_t Dh = S | (S << 1) | (S >> 1);
-        const uint64_t Dv = Dh | wave_shr1(Dh) | wave_shl1(Dh);
-        const uint64_t Fn = Fr | (Dv & allow);
-        const bool changed = __ballot(Fn != Fr) != 0ull;
-        Fr = Fn;
-        if (!changed) break;
-      }
-      rev |= Fr;
-      newly = (uint32_t)__popcll(Fr);
-    }
-  }
+  board_click(rng, mine, rev, fc, cell, p, J, sTab, sR, g, lane, done, outcome, newly, total_rev, mines_changed);
   STAMP(3);
-  // one reduction for both counts: total revealed (hi 16) | newly revealed (lo 16)
-  const uint32_t packed = wave_sum(((uint32_t)__popcll(rev) << 16) | newly);
-  const uint32_t total_rev = packed >> 16;
-  newly = packed & 0xffffu;
-  if (!cell_rev && outcome != MS_OUTCOME_LOSS && (int)total_rev >= A - p.K) {
-    done = true;
-    outcome = MS_OUTCOME_WIN;
-    reward += p.win_reward;
-  }
+  if (outcome == MS_OUTCOME_LOSS) reward += p.loss_reward;
+  if (outcome == MS_OUTCOME_WIN) reward += p.win_reward;
   reward -= p.step_penalty;
   step_count += 1;
 
@@ -935,6 +951,138 @@ __global__ __launch_bounds__(64) void k_tape(const uint64_t* mw, const uint64_t*
     act = (int64_t)src * W + col;
   }
   if (lane == 0) actions[env] = act;
+}
+
+
+// ---------------------------------------------------------------------------
+// Late-start resets (VecMinesweeper._apply_late_start, env.py:416-466).
+// The reference draws every late start from ONE generator shared by all envs, in
+// env order, and each env consumes a data-dependent number of draws, so the envs
+// form a sequential chain: one wave walks them in order (each board's clicks are
+// still wave-parallel: placement + flood fill as in k_step). Only envs flagged in
+// `need` (the step's dones; all envs on ms_reset) are visited.
+// ---------------------------------------------------------------------------
+struct LateCfg {
+  double prob;
+  int32_t min_hidden, max_hidden, max_attempts, max_extra_steps;
+};
+
+template <int H_, int W_>
+__global__ __launch_bounds__(64) void k_late(KParams p, Pcg* lstate, LateCfg lc, const uint8_t* need) {
+  __shared__ uint64_t sR[kWave];
+  __shared__ uint64_t sM[kWave + 2];
+  __shared__ uint32_t sTab[(H_ && W_) ? H_ * W_ : kMaxH * kMaxW];
+  const int lane = lane_id();
+  const Geo<H_, W_> g(p.H, p.W);
+  const int H = g.H, W = g.W, A = g.A(), NW = g.NW();
+  const uint64_t rowmask = g.rowmask();
+  const int safe_total = A - p.K;
+  Pcg L;
+  L.hi = lstate->hi;
+  L.lo = lstate->lo;
+  L.ihi = lstate->ihi;
+  L.ilo = lstate->ilo;
+  L.has32 = lstate->has32;
+  L.uinteger = lstate->uinteger;
+  uint64_t J[4];
+  {
+    const ulonglong2* e = reinterpret_cast<const ulonglong2*>(p.jump + 4 * lane);
+    const ulonglong2 a0 = e[0], a1 = e[1];
+    J[0] = a0.x;
+    J[1] = a0.y;
+    J[2] = a1.x;
+    J[3] = a1.y;
+  }
+  for (int64_t env = 0; env < p.n; ++env) {
+    if (need && !need[env]) continue;
+    EnvMeta* mp = p.meta + env;
+    uint64_t* mwords = p.mine_words + env * NW;
+    uint64_t* rwords = p.rev_words + env * NW;
+    uint64_t mine = load_row(mwords, g, lane);
+    uint64_t rev = load_row(rwords, g, lane);
+    Pcg rng;
+    rng.hi = rfl64(mp->st_hi);
+    rng.lo = rfl64(mp->st_lo);
+    rng.ihi = rfl64(mp->inc_hi);
+    rng.ilo = rfl64(mp->inc_lo);
+    rng.has32 = rfl(mp->has32);
+    rng.uinteger = rfl(mp->uinteger);
+    int32_t step_count = (int32_t)rfl((uint32_t)mp->step_count);
+    bool fc = (rfl(mp->flags) & 1u) != 0;
+    // prob <= 0 short-circuits before the draw (env.py:421)
+    if (lc.prob > 0.0 && (double)(pcg_next64(L) >> 11) * 0x1.0p-53 < lc.prob) {
+      bool success = false;
+      for (int att = 0; att < lc.max_attempts && !success; ++att) {
+        if (fc) {  // env.reset() (env.py:87-101): the env's own RNG continues
+          mine = 0ull;
+          rev = 0ull;
+          fc = false;
+          step_count = 0;
+        }
+        const int first = (int)pcg_bounded(L, (uint32_t)(A - 1));
+        bool done, mc = false;
+        int oc;
+        uint32_t nw, tr;
+        board_click(rng, mine, rev, fc, first, p, J, sTab, sR, g, lane, done, oc, nw, tr, mc);
+        step_count += 1;
+        if (done) continue;
+        int target = lc.min_hidden + (int)pcg_bounded(L, (uint32_t)(lc.max_hidden - lc.min_hidden));
+        target = target < safe_total ? target : safe_total;
+        target = target > 1 ? target : 1;
+        int revealed = (int)tr;
+        for (int k = 0; k < lc.max_extra_steps; ++k) {
+          if (safe_total - revealed <= target) {
+            success = true;
+            break;
+          }
+          const uint64_t cand = ~mine & ~rev & (lane < H ? rowmask : 0ull);
+          const uint32_t pc = (uint32_t)__popcll(cand);
+          const uint32_t cnt = wave_sum(pc);
+          if (cnt == 0) break;
+          const uint32_t kk = pcg_bounded(L, cnt - 1u);  // rng.choice(flatnonzero(...)) (row-major)
+          const uint32_t before = wave_excl_scan(pc);
+          const bool mine_lane = kk >= before && kk < before + pc;
+          const uint64_t who = __ballot(mine_lane);
+          const int src = __ffsll((unsigned long long)who) - 1;
+          const int col = (int)readlane32((uint32_t)(mine_lane ? select_bit(cand, kk - before) : 0), src);
+          board_click(rng, mine, rev, fc, src * W + col, p, J, sTab, sR, g, lane, done, oc, nw, tr, mc);
+          step_count += 1;
+          revealed = (int)tr;
+          if (done) break;
+        }
+        if (!success && !done && safe_total - revealed <= target) success = true;
+      }
+      if (!success) {  // fallback: leave the board fresh (env.py:465-466)
+        mine = 0ull;
+        rev = 0ull;
+        fc = false;
+        step_count = 0;
+      }
+    }
+    if (lane == 0) {
+      mp->st_hi = rng.hi;
+      mp->st_lo = rng.lo;
+      mp->has32 = rng.has32;
+      mp->uinteger = rng.uinteger;
+      mp->step_count = step_count;
+      mp->flags = fc ? 1u : 0u;
+    }
+    store_rows(mwords, mine, sR, g, lane);
+    store_rows(rwords, rev, sR, g, lane);
+    __syncthreads();
+    if (p.obs || p.mask) {
+      stage_rows(sR, sM, rev, mine, g, lane);
+      emit_obs(p.obs ? p.obs + env * 10 * A : nullptr, p.mask ? p.mask + env * A : nullptr, sR, sM, fc, g,
+               lane);
+    }
+    __syncthreads();
+  }
+  if (lane == 0) {
+    lstate->hi = L.hi;
+    lstate->lo = L.lo;
+    lstate->has32 = L.has32;
+    lstate->uinteger = L.uinteger;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1136,6 +1284,9 @@ struct ms_handle {
   uint64_t* jump;  // [64][4] PCG64 jump-ahead table (device)
   uint64_t* diag;  // optional stamp buffer (MS_DIAG builds)
   uint32_t dbg_flags;
+  int late_on;     // ms_set_late_start called with prob > 0
+  LateCfg late;
+  Pcg* late_rng;   // device: the shared late-start generator
 };
 
 namespace {
@@ -1148,6 +1299,36 @@ bool shape_ok(const ms_cfg* c) {
 template <int H_, int W_>
 void launch_step(const KParams& p, hipStream_t s) {
   hipLaunchKernelGGL((k_step<H_, W_>), dim3((unsigned)p.n), dim3(64), 0, s, p);
+}
+
+template <int H_, int W_>
+void launch_late_t(const KParams& p, Pcg* st, const LateCfg& c, const uint8_t* need, hipStream_t s) {
+  hipLaunchKernelGGL((k_late<H_, W_>), dim3(1), dim3(64), 0, s, p, st, c, need);
+}
+
+void fill_params(const ms_handle* h, KParams& p) {
+  p.meta = h->meta;
+  p.mine_words = h->mine_words;
+  p.rev_words = h->rev_words;
+  p.n = h->n;
+  p.H = h->H;
+  p.W = h->W;
+  p.K = h->cfg.mine_count;
+  p.guarantee = h->cfg.guarantee_safe_neighborhood ? 1 : 0;
+  p.win_reward = h->cfg.win_reward;
+  p.loss_reward = h->cfg.loss_reward;
+  p.step_penalty = h->cfg.step_penalty;
+  p.jump = h->jump;
+  p.diag = h->diag;
+  p.dbg_flags = h->dbg_flags;
+}
+
+int launch_late(const ms_handle* h, const KParams& p, const uint8_t* need, hipStream_t s) {
+  if (h->H == 16 && h->W == 16) launch_late_t<16, 16>(p, h->late_rng, h->late, need, s);
+  else if (h->H == 9 && h->W == 9) launch_late_t<9, 9>(p, h->late_rng, h->late, need, s);
+  else launch_late_t<0, 0>(p, h->late_rng, h->late, need, s);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? MS_OK : hip_fail(e, "late-start launch");
 }
 
 int do_step(ms_handle* h, const void* actions, int i32, float* obs, uint8_t* mask, float* reward,
@@ -1164,22 +1345,10 @@ int do_step(ms_handle* h, const void* actions, int i32, float* obs, uint8_t* mas
   p.last_new = last_new;
   p.frac = frac;
   p.outcome = outcome;
-  p.meta = h->meta;
-  p.mine_words = h->mine_words;
-  p.rev_words = h->rev_words;
-  p.n = h->n;
-  p.H = h->H;
-  p.W = h->W;
-  p.K = h->cfg.mine_count;
-  p.guarantee = h->cfg.guarantee_safe_neighborhood ? 1 : 0;
+  fill_params(h, p);
   p.actions_i32 = i32;
-  p.win_reward = h->cfg.win_reward;
-  p.loss_reward = h->cfg.loss_reward;
-  p.step_penalty = h->cfg.step_penalty;
-  p.jump = h->jump;
-  p.diag = h->diag;
-  p.dbg_flags = h->dbg_flags;
   hipStream_t s = (hipStream_t)stream;
+  if (h->late_on && !done) return fail(MS_EINVAL, "ms_step: late start needs the done output");
   if (h->H == 16 && h->W == 16) launch_step<16, 16>(p, s);
   else if (h->H == 9 && h->W == 9) launch_step<9, 9>(p, s);
   else if (h->H == 30 && h->W == 16) launch_step<30, 16>(p, s);
@@ -1188,6 +1357,8 @@ int do_step(ms_handle* h, const void* actions, int i32, float* obs, uint8_t* mas
   else launch_step<0, 0>(p, s);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "ms_step launch");
+  // auto-resets that draw a late start (env.py:497-498 -> 406-414), in env order
+  if (h->late_on) return launch_late(h, p, done, s);
   return MS_OK;
 }
 
@@ -1279,6 +1450,7 @@ int ms_destroy(ms_handle* h) {
   if (h->mine_words) (void)hipFree(h->mine_words);
   if (h->rev_words) (void)hipFree(h->rev_words);
   if (h->jump) (void)hipFree(h->jump);
+  if (h->late_rng) (void)hipFree(h->late_rng);
   delete h;
   return MS_OK;
 }
@@ -1305,7 +1477,60 @@ int ms_reset(ms_handle* h, float* obs, uint8_t* mask, void* stream) {
   hipLaunchKernelGGL(k_reset, dim3(blocks), dim3(256), 0, (hipStream_t)stream, h->meta, h->mine_words,
                      h->rev_words, h->n, h->NW, obs, mask, h->A);
   hipError_t e = hipGetLastError();
-  return e == hipSuccess ? MS_OK : hip_fail(e, "ms_reset launch");
+  if (e != hipSuccess) return hip_fail(e, "ms_reset launch");
+  if (h->late_on) {  // every env: _reset_env_state (env.py:406-414, 468-477)
+    KParams p = {};
+    fill_params(h, p);
+    p.obs = obs;
+    p.mask = mask;
+    return launch_late(h, p, nullptr, (hipStream_t)stream);
+  }
+  return MS_OK;
+}
+
+int ms_set_late_start(ms_handle* h, double prob, int32_t min_hidden, int32_t max_hidden, int32_t max_attempts,
+                      int32_t max_extra_steps, uint64_t late_seed) {
+  if (!h) return fail(MS_EINVAL, "ms_set_late_start: null handle");
+  // clamps of env.py:424-430
+  LateCfg c;
+  c.prob = prob;
+  c.min_hidden = min_hidden < 1 ? 1 : min_hidden;
+  c.max_hidden = max_hidden < c.min_hidden ? c.min_hidden : max_hidden;
+  c.max_attempts = max_attempts < 1 ? 1 : max_attempts;
+  c.max_extra_steps = max_extra_steps < 1 ? 1 : max_extra_steps;
+  HostPcg r;
+  host_seed(r, late_seed);
+  Pcg d;
+  d.hi = (uint64_t)(r.state >> 64);
+  d.lo = (uint64_t)r.state;
+  d.ihi = (uint64_t)(r.inc >> 64);
+  d.ilo = (uint64_t)r.inc;
+  d.has32 = (uint32_t)r.has32;
+  d.uinteger = r.uinteger;
+  if (!h->late_rng) {
+    hipError_t e = hipMalloc(&h->late_rng, sizeof(Pcg));
+    if (e != hipSuccess) return hip_fail(e, "ms_set_late_start alloc");
+  }
+  hipError_t e = hipMemcpy(h->late_rng, &d, sizeof(Pcg), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(e, "ms_set_late_start copy");
+  h->late = c;
+  h->late_on = 1;
+  return MS_OK;
+}
+
+int ms_late_rng_state(ms_handle* h, uint64_t* out) {
+  if (!h || !out) return fail(MS_EINVAL, "ms_late_rng_state: bad argument");
+  if (!h->late_rng) return fail(MS_EINVAL, "ms_late_rng_state: late start not configured");
+  Pcg d;
+  hipError_t e = hipMemcpy(&d, h->late_rng, sizeof(Pcg), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_fail(e, "ms_late_rng_state copy");
+  out[0] = d.hi;
+  out[1] = d.lo;
+  out[2] = d.ihi;
+  out[3] = d.ilo;
+  out[4] = d.has32;
+  out[5] = d.uinteger;
+  return MS_OK;
 }
 
 int ms_step(ms_handle* h, const int64_t* actions, float* obs, uint8_t* mask, float* reward, uint8_t* done,

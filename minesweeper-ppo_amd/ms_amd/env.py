@@ -169,9 +169,6 @@ class VecMinesweeper:
                  late_start_seed: Optional[int] = None, *, device=None,
                  shard: Tuple[int, int] = (0, 1), as_numpy: bool = False):
         assert num_envs > 0  # env.py:390
-        if late_start_cfg and float(late_start_cfg.get("prob", 0.0)) > 0.0:
-            raise NotImplementedError(
-                "late_start is not implemented on the HIP path yet (SURVEY.md §8f rank 3)")
         rank, world = shard
         assert 0 <= rank < world and world <= num_envs
         self.cfg = cfg
@@ -194,6 +191,21 @@ class VecMinesweeper:
             L.check(self._lib.ms_create(ctypes.byref(c), self.num_envs_total, int(seed), begin,
                                         self.num_envs, ctypes.byref(h)))
         self._h = h
+        # late start (env.py:397-403): one generator for all envs, seeded late_start_seed
+        # or, as the reference, with the base generator's next draw after the N seeds
+        self._late_start_cfg = dict(late_start_cfg) if late_start_cfg else None
+        if self._late_start_cfg:
+            if late_start_seed is None:
+                base = np.random.default_rng(seed)
+                base.integers(0, 2**31 - 1, size=self.num_envs_total, dtype=np.int64)
+                late_start_seed = int(base.integers(0, 2**31 - 1))
+            ls = self._late_start_cfg
+            mn = int(ls.get("min_hidden", 5))
+            # a shard cannot replay the global env-order stream: it draws its own
+            lseed = int(late_start_seed) if world == 1 else (int(late_start_seed) * 1000003 + begin) % 2**63
+            L.check(self._lib.ms_set_late_start(h, float(ls.get("prob", 0.0)), mn, int(ls.get("max_hidden", mn)),
+                                                int(ls.get("max_attempts", 3)),
+                                                int(ls.get("max_extra_steps", self.A)), lseed))
         self._version = 0
         self._snap = None
         self._snap_version = -1
@@ -294,6 +306,13 @@ class VecMinesweeper:
     def set_debug_flags(self, flags: int) -> None:
         """msenv_debug.h hooks (tests): e.g. L.MS_DBG_FORCE_SERIAL_PLACEMENT."""
         L.check(self._lib.ms_set_debug_flags(self._h, int(flags)))
+
+    def late_rng_state(self) -> np.ndarray:
+        """The shared late-start generator's state u64[6] (ms_rng_state layout)."""
+        out = np.zeros(6, dtype=np.uint64)
+        torch.cuda.synchronize(self.device)
+        L.check(self._lib.ms_late_rng_state(self._h, out.ctypes.data))
+        return out
 
     def rng_state(self) -> np.ndarray:
         out = torch.empty((self.num_envs, 6), dtype=torch.int64, device=self.device)

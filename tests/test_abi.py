@@ -11,12 +11,13 @@ import pytest
 from conftest import ROOT
 
 HEADERS = [os.path.join(ROOT, "include", h) for h in ("msenv.h", "msenv_debug.h")]
+CNN_HEADER = os.path.join(ROOT, "include", "mscnn.h")
 
 
-def header_functions():
-    src = "".join(open(h).read() for h in HEADERS)
+def header_functions(headers=HEADERS, prefix="ms_"):
+    src = "".join(open(h).read() for h in headers)
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(ms_[a-z0-9_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(" + prefix + r"[a-z0-9_]+)\s*\(", src)))
 
 
 def test_header_declares_expected_entry_points():
@@ -33,6 +34,29 @@ def test_library_exports_every_header_symbol():
     for name in header_functions():
         assert hasattr(lib, name), name
         assert name in L.SIGNATURES, f"{name} has no ctypes signature"
+
+
+def test_library_exports_every_cnn_header_symbol():
+    from ms_amd import _lib as L
+    lib = L.load()
+    fns = header_functions([CNN_HEADER], "mc_")
+    assert {"mc_conv_gn_fwd", "mc_conv_gn_bwd", "mc_conv_gn_bwd_workspace", "mc_heads_fwd", "mc_heads_bwd",
+            "mc_heads_bwd_workspace", "mc_last_error"} <= set(fns)
+    for name in fns:
+        assert hasattr(lib, name), name
+
+
+def test_cnn_entry_points_validate_arguments():
+    from ms_amd import _lib as L
+    lib = L.load()
+    lib.mc_last_error.restype = ctypes.c_char_p
+    lib.mc_conv_gn_bwd_workspace.restype = ctypes.c_int64
+    assert lib.mc_conv_gn_bwd_workspace(0, 16, 16, 96) == -1
+    assert lib.mc_conv_gn_bwd_workspace(4, 16, 16, 32) == -1  # cin 16 or 96 only
+    vp = ctypes.c_void_p
+    lib.mc_conv_gn_fwd.argtypes = [vp] * 10 + [ctypes.c_int32] * 4 + [ctypes.c_float, vp]
+    assert lib.mc_conv_gn_fwd(*([None] * 10), 4, 16, 16, 96, 1e-5, None) == 1
+    assert b"bad argument" in lib.mc_last_error()
 
 
 def test_single_hip_runtime_mapped():

@@ -21,11 +21,17 @@ def _codes(obs: torch.Tensor) -> np.ndarray:
     return O.codes_from_obs(obs.cpu().numpy())
 
 
-@pytest.mark.parametrize("name", [n for n in golden_files("traj_*.npz") if "late" not in n])
+@pytest.mark.parametrize("name", golden_files("traj_*.npz"))
 def test_trajectory_golden_gpu(gpu, name):
+    """Reference trajectories replayed bit-exact, incl. late-start resets (traj_*_late:
+    VecMinesweeper(late_start_cfg, late_start_seed=seed+1) as train_rl.py:350-361)."""
     z = golden(name)
     H, W, K, N, T = (int(z[k]) for k in ("H", "W", "K", "N", "T"))
-    v = _vec(H, W, K, N, seed=int(z["seed"]))
+    late = None
+    if "late_prob" in z.files:
+        late = dict(prob=float(z["late_prob"]), min_hidden=int(z["late_min"]), max_hidden=int(z["late_max"]))
+    v = _vec(H, W, K, N, seed=int(z["seed"]), late_start_cfg=late,
+             late_start_seed=int(z["seed"]) + 1 if late else None)
     d = v.reset()
     assert np.array_equal(_codes(d["obs"]), z["reset_codes"])
     mode = int(z["mode"])
@@ -45,11 +51,13 @@ def test_trajectory_golden_gpu(gpu, name):
         mines = v.snapshot_tensors()["mine"].cpu().numpy().reshape(N, -1)
         assert np.array_equal(np.packbits(mines, axis=1), z["mines"][t]), t
     assert np.array_equal(v.rng_state(), z["end_states"])
+    if late:
+        assert np.array_equal(v.late_rng_state(), z["late_state"])
 
 
-def _diff_run(H, W, K, N, T, mode, seed=0, check_every=1, labels=True):
-    v = _vec(H, W, K, N, seed=seed)
-    o = O.OracleVec(H, W, K, N, seed=seed)
+def _diff_run(H, W, K, N, T, mode, seed=0, check_every=1, labels=True, late=None):
+    v = _vec(H, W, K, N, seed=seed, late_start_cfg=late, late_start_seed=seed + 1 if late else None)
+    o = O.OracleVec(H, W, K, N, seed=seed, late_start=late, late_seed=seed + 1 if late else None)
     d = v.reset()
     oo, om = o.reset()
     assert np.array_equal(d["obs"].cpu().numpy(), oo)
@@ -78,6 +86,14 @@ def _diff_run(H, W, K, N, T, mode, seed=0, check_every=1, labels=True):
     assert np.array_equal(snap["mine"].cpu().numpy().reshape(N, -1), osnap["mine"])
     assert np.array_equal(snap["step_count"].cpu().numpy(), osnap["step_count"])
     assert np.array_equal(v.rng_state(), o.rng_state())
+
+
+@pytest.mark.parametrize("H,W,K,N", [(16, 16, 40, 96), (9, 9, 10, 200), (30, 16, 99, 40), (7, 11, 20, 64)])
+def test_late_start_matches_oracle(gpu, H, W, K, N):
+    """Late-start resets (env.py:416-466) on the HIP path vs the C oracle: the shared
+    generator's env-order chain, retries, fallback resets, step counts."""
+    late = dict(prob=0.6, min_hidden=3, max_hidden=2 * K, max_attempts=2)
+    _diff_run(H, W, K, N, T=60, mode=1, seed=5, check_every=3, labels=False, late=late)
 
 
 @pytest.mark.parametrize("H,W,K", [(16, 16, 40), (9, 9, 10), (30, 16, 99), (16, 30, 99), (8, 8, 10)])

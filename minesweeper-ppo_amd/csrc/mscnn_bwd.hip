@@ -115,9 +115,15 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
         if (i < NCH) yr[i] = u32x4{0u, 0u, 0u, 0u};
         if (i < NCH && gact && px < P) {
           const size_t o = ((size_t)n * P + px) * COUT + c8 * 8;
+#ifndef MC_EXP_B_NO_P1LOAD
           dv[u] = *reinterpret_cast<const u32x4*>(&p.dout[o]);
           ov[u] = *reinterpret_cast<const u32x4*>(&p.out[o]);
           yr[i] = *reinterpret_cast<const u32x4*>(&p.y[o]);
+#else
+          dv[u] = u32x4{(unsigned)o, 1u, 2u, 3u};
+          ov[u] = u32x4{(unsigned)o, 5u, 2u, 3u};
+          yr[i] = u32x4{(unsigned)o, 7u, 2u, 3u};
+#endif
         }
       }
 #pragma unroll
@@ -210,7 +216,9 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
           for (int j = 0; j < 8; ++j) d8[j] = (__bf16)(A[j] * (float)z8[j] + Bg * (float)y8[j] + Cg);
           const u32x4 v = __builtin_bit_cast(u32x4, d8);
           *reinterpret_cast<u32x4*>(&sD[px * DCP + c8 * 8]) = v;
+#ifndef MC_EXP_B_NO_DYSTORE
           *reinterpret_cast<u32x4*>(&p.dy[((size_t)n * P + px) * COUT + c8 * 8]) = v;
+#endif
         }
       }
     }
@@ -234,7 +242,11 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
       for (int ct = 0; ct < 3; ++ct)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[t][ct][i] = 0.f;
+#ifdef MC_EXP_B_NO_DGRAD
+    for (int tap = 0; tap < 0; ++tap) {
+#else
     for (int tap = 0; tap < 9; ++tap) {
+#endif
       if (tap + 1 < 9) {
         const u32x4* ws = reinterpret_cast<const u32x4*>(p.wT + (size_t)(tap + 1) * COUT * COUT);
 #pragma unroll
@@ -305,7 +317,9 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
           bf16x8 s8;
 #pragma unroll
           for (int j = 0; j < 8; ++j) s8[j] = (__bf16)((float)a8[j] + (float)r8[j]);
+#ifndef MC_EXP_B_NO_EPI
           *reinterpret_cast<u32x4*>(&p.dx[((size_t)n * P + px) * COUT + c8 * 8]) = __builtin_bit_cast(u32x4, s8);
+#endif
         }
       }
     }

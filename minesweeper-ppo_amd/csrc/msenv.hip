@@ -620,6 +620,7 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
 // ---------------------------------------------------------------------------
 // ms_step: one wave = one env.
 // ---------------------------------------------------------------------------
+
 #ifdef MS_DIAG
 #define STAMP(k)                                                              \
   do {                                                                        \
@@ -643,7 +644,7 @@ __device__ __forceinline__ void board_click(Pcg& rng, uint64_t& mine, uint64_t& 
                                             const KParams& p, const uint64_t (&J)[4], uint32_t* sTab,
                                             uint64_t* sR, const Geo<H_, W_>& g, int lane, bool& done,
                                             int& outcome, uint32_t& newly, uint32_t& total_rev,
-                                            bool& mines_changed) {
+                                            bool& mines_changed, int64_t env = -1) {
   const int H = g.H, W = g.W, A = g.A();
   const uint64_t rowmask = g.rowmask();
   const int ar = cell / W, ac = cell - (cell / W) * W;
@@ -665,6 +666,7 @@ __device__ __forceinline__ void board_click(Pcg& rng, uint64_t& mine, uint64_t& 
       fc = true;
       mines_changed = true;
     }
+    if (env >= 0) STAMP(2);
     const bool hit = (readlane64(mine, ar) >> ac) & 1ull;
     if (hit) {
       if (lane == ar) rev |= 1ull << ac;
@@ -751,7 +753,8 @@ __global__ __launch_bounds__(64) void k_step(KParams p) {
   int outcome = MS_OUTCOME_NONE;
   uint32_t newly = 0, total_rev = 0;
   bool mines_changed = false;
-  board_click(rng, mine, rev, fc, cell, p, J, sTab, sR, g, lane, done, outcome, newly, total_rev, mines_changed);
+  board_click(rng, mine, rev, fc, cell, p, J, sTab, sR, g, lane, done, outcome, newly, total_rev, mines_changed,
+              env);
   STAMP(3);
   if (outcome == MS_OUTCOME_LOSS) reward += p.loss_reward;
   if (outcome == MS_OUTCOME_WIN) reward += p.win_reward;

@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 PKG=minesweeper-ppo_amd
 SRCS="$PKG/csrc/msenv.hip $PKG/csrc/mscnn.hip $PKG/csrc/mscnn_bwd.hip $PKG/csrc/msheads.hip"
-for v in base NO_EPI NO_WLOAD NO_STATS NO_IN NO_MFMA; do
+for v in ${VARIANTS:-base NO_EPI NO_WLOAD NO_STATS NO_IN NO_MFMA}; do
   so=/tmp/libmsenv_exp_$v.so
   D=""; [ $v != base ] && D="-DMC_EXP_$v"
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $D -shared -o $so $SRCS || exit 1

@@ -21,6 +21,7 @@
 
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "../../include/msenv.h"
 #include "../../include/mscnn.h"
@@ -60,6 +61,7 @@ struct FwdParams {
   float* stats;
   int N, H, W;
   float eps;
+  unsigned long long* diag;  // MC_DIAG builds: per-workgroup phase cycle totals [grid][8]
 };
 
 // LDS layout (bf16 elements):
@@ -76,6 +78,59 @@ template <int CIN>
 __host__ __device__ inline int region0_elems(int H, int W) {
   const int a = (H * W + 1) * cinp<CIN>(), b = H * W * COUT;
   return ((a > b ? a : b) + 7) & ~7;
+}
+
+#ifdef MC_DIAG
+#define FSTAMP(k)                                      \
+  do {                                                 \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    dacc[k] += t_ - tlast;                             \
+    tlast = t_;                                        \
+  } while (0)
+#else
+#define FSTAMP(k) do { } while (0)
+#endif
+
+// s_waitcnt vmcnt(n) for a wave-uniform n (the immediate must be a constant)
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  switch (n) {
+#define MC_VMW(k) \
+  case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    MC_VMW(0) MC_VMW(1) MC_VMW(2) MC_VMW(3) MC_VMW(4) MC_VMW(5) MC_VMW(6) MC_VMW(7) MC_VMW(8) MC_VMW(9)
+    MC_VMW(10) MC_VMW(11) MC_VMW(12) MC_VMW(13) MC_VMW(14) MC_VMW(15) MC_VMW(16) MC_VMW(17) MC_VMW(18)
+    MC_VMW(19) MC_VMW(20) MC_VMW(21) MC_VMW(22) MC_VMW(23) MC_VMW(24) MC_VMW(25) MC_VMW(26) MC_VMW(27)
+    MC_VMW(28) MC_VMW(29) MC_VMW(30) MC_VMW(31) MC_VMW(32) MC_VMW(33) MC_VMW(34) MC_VMW(35) MC_VMW(36)
+#undef MC_VMW
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+// One weight tap [96][96] global -> LDS by LDS-DMA (global_load_lds_dwordx4: each
+// wave-instruction writes 1 KiB lane-linearly). The LDS image is unpadded with 16-B
+// chunk ch of row co stored at ch ^ ((co >> 2) & 3) (conflict-free B reads); the
+// swizzle is applied on the SOURCE address. 18 wave-instructions per tap, split
+// over the 4 waves (5/5/4/4).
+#define MC_GLDS_W(T_, dst_)                                                                      \
+  do {                                                                                           \
+    for (int j_ = wave; j_ < 18; j_ += 4) {                                                      \
+      const int o_ = 1024 * j_ + 16 * lane;                                                      \
+      const int co_ = o_ / 192, ch_ = ((o_ % 192) >> 4) ^ ((co_ >> 2) & 3);                    \
+      glds16(p.wt + ((size_t)(T_) * COUT + co_) * COUT + ch_ * 8,                               \
+             reinterpret_cast<unsigned char*>(dst_) + 1024 * j_);                                \
+    }                                                                                            \
+  } while (0)
+
+// global_load_lds_dwordx4 through inline asm: hipcc does not track it, so it inserts no
+// vmcnt(0) before the next LDS read (the builtin makes it drain the DMA there); the
+// kernel retires it with counted waits (wait_vmcnt). M0 is saved and restored in the
+// statement (cdna_hip_programming.md, LDS-DMA recipe).
+__device__ __forceinline__ void glds16(const void* gsrc, void* lds_dst) {
+  const unsigned dst = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)lds_dst;
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(dst))
+               : "memory");
 }
 
 // (macros rather than lambdas: captured register arrays would be demoted to scratch)
@@ -107,8 +162,11 @@ __host__ __device__ inline int region0_elems(int H, int W) {
     }                                                                                   \
   } while (0)
 
-template <int CIN, int NPT, bool FULL>
-__global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams p) {
+// PF = true: one workgroup per CU with the registers to prefetch the next sample's
+// input and this sample's residual, double-buffered weight taps (one barrier per
+// tap). PF = false: two workgroups per CU, nothing held across phases.
+template <int CIN, int NPT, bool FULL, bool PF>
+__global__ __launch_bounds__(256, PF ? 1 : (NPT <= 2 ? 2 : 1)) void k_conv_gn_fwd(FwdParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int CINP = cinp<CIN>();
   constexpr int C8 = CIN / 8;
@@ -118,7 +176,14 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
   __bf16* sX = reinterpret_cast<__bf16*>(smem);
   __bf16* sO = sX;
   __bf16* sW = sX + region0_elems<CIN>(H, W);
-  float* sRed = reinterpret_cast<float*>(sW + COUT * CINP);
+  // GL: the PF path's weight taps arrive by LDS-DMA into a ring of 3 unpadded buffers,
+  // two taps ahead of the MFMAs (raw barriers + counted vmcnt keep them in flight)
+#ifdef MC_FWD_GL
+  constexpr bool GL = PF && CIN == 96;
+#else
+  constexpr bool GL = false;  // measured slower (2.87 vs 2.50 ms): per-CU LDS-DMA rate, see DESIGN.md §5
+#endif
+  float* sRed = reinterpret_cast<float*>(sW + (GL ? 3 * COUT * COUT : (PF ? 2 : 1) * COUT * CINP));
   float* sGB = sRed + WAVES * NGRP;  // [gamma | beta]
   float* sAB = sGB + 2 * COUT;        // per sample: [scale | shift | dropout scale]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -136,15 +201,27 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
     qc[t] = q < P ? q - qr[t] * W : -1000;
   }
   u32x4 wr[NWC];
+  u32x4 xin[NPF];
+  constexpr int NEC = (NPT * 128 * (COUT / 8) + 255) / 256;  // 16-B output chunks per thread
+  u32x4 rv[PF ? NEC : 1];
+  if (PF && (int)blockIdx.x < p.N) MC_LOAD_IN(blockIdx.x, xin);
+  int gi = 0;  // GL: running tap count -> ring slot gi % 3
+  const int nglds = (18 - wave + 3) / 4;  // this wave's LDS-DMA instructions per tap
+  if (GL && (int)blockIdx.x < p.N) {
+    MC_GLDS_W(0, sW);
+    MC_GLDS_W(1, sW + COUT * COUT);
+  }
+#ifdef MC_DIAG
+  unsigned long long dacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tlast = __builtin_amdgcn_s_memtime();
+#endif
   for (int n = blockIdx.x; n < p.N; n += gridDim.x) {
     // loop-variant copy of tid: keeps the per-chunk address math inside the loop instead of
     // hoisting a dozen 64-bit addresses out of it (they would be spilled)
     const int tid = threadIdx.x + opaque0();
-    // ---- stage the input tile (the zero row is re-written: the epilogue reuses region0).
-    // No cross-sample register prefetch: the CU's other workgroup computes meanwhile. ----
-    u32x4 xin[NPF];
+    // ---- stage the input tile (the zero row is re-written: the epilogue reuses region0) ----
 #ifndef MC_EXP_NO_IN
-    MC_LOAD_IN(n, xin);
+    if (!PF) MC_LOAD_IN(n, xin);  // PF: prefetched during the previous sample's last tap
 #else
     for (int k = 0; k < NPF; ++k) xin[k] = u32x4{1u, 2u, 3u, (unsigned)n};
 #endif
@@ -157,9 +234,13 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
         *reinterpret_cast<u32x4*>(&sX[px * CINP + c8 * 8]) = xin[k];
       }
     }
-    MC_LOAD_W(0, wr);
-    MC_STORE_W(0, wr);
+    if (!GL) {
+      MC_LOAD_W(0, wr);
+      MC_STORE_W(0, wr);
+    }
+    const int nn = n + gridDim.x;
     __syncthreads();
+    FSTAMP(0);  // stage input + tap-0 weights
 
     f32x16 acc[NPT][3];
 #pragma unroll
@@ -171,8 +252,21 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
 
     for (int tap = 0; tap < 9; ++tap) {
 #ifndef MC_EXP_NO_WLOAD
-      if (tap + 1 < 9) MC_LOAD_W(tap + 1, wr);
+      if (!GL && tap + 1 < 9) MC_LOAD_W(tap + 1, wr);
 #endif
+      if (GL) MC_GLDS_W((tap + 2) % 9, sW + ((gi + 2) % 3) * COUT * COUT);  // next sample's taps 0/1 at 7/8
+      if (PF && tap == 8) {
+        // vmcnt retires in issue order: these are issued after the last weight wait,
+        // in the order they are consumed (residual in this epilogue, input next sample)
+#pragma unroll
+        for (int k = 0; k < (PF ? NEC : 0); ++k) {
+          const int c = tid + 256 * k;
+          rv[k] = u32x4{0u, 0u, 0u, 0u};
+          if (p.res && c < P * (COUT / 8)) rv[k] = *reinterpret_cast<const u32x4*>(&p.res[(size_t)n * P * COUT + c * 8]);
+        }
+        if (nn < p.N) MC_LOAD_IN(nn, xin);
+      }
+      const __bf16* sWt = GL ? sW + (gi % 3) * COUT * COUT : sW + (PF ? (tap & 1) : 0) * COUT * CINP;
       const int dr = tap / 3 - 1, dc = tap % 3 - 1;
       int aoff[NPT];
 #pragma unroll
@@ -184,28 +278,69 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
 #ifdef MC_EXP_NO_MFMA
       if (p.N < 0)
 #endif
+      if constexpr (PF) {
+        // all of this tap's LDS operand reads first (in k-step order), then the MFMAs:
+        // with one wave per SIMD nothing else hides a read -> use latency
+        constexpr int KS = CIN / 16;
+        bf16x8 bq[KS][3], aq[KS][NPT];
 #pragma unroll
-      for (int k0 = 0; k0 < CIN; k0 += 16) {
-        bf16x8 b[3];
+        for (int ks = 0; ks < KS; ++ks) {
 #pragma unroll
-        for (int ct = 0; ct < 3; ++ct)
-          b[ct] = *reinterpret_cast<const bf16x8*>(&sW[(ct * 32 + l32) * CINP + k0 + 8 * hh]);
+          for (int ct = 0; ct < 3; ++ct)
+            bq[ks][ct] = GL ? *reinterpret_cast<const bf16x8*>(
+                                  &sWt[(ct * 32 + l32) * COUT + 8 * ((2 * ks + hh) ^ (((ct * 32 + l32) >> 2) & 3))])
+                            : *reinterpret_cast<const bf16x8*>(&sWt[(ct * 32 + l32) * CINP + ks * 16 + 8 * hh]);
 #pragma unroll
-        for (int t = 0; t < NPT; ++t) {
-          const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sX[aoff[t] + k0]);
+          for (int t = 0; t < NPT; ++t) aq[ks][t] = *reinterpret_cast<const bf16x8*>(&sX[aoff[t] + ks * 16]);
+        }
 #pragma unroll
-          for (int ct = 0; ct < 3; ++ct) acc[t][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[ct], acc[t][ct], 0, 0, 0);
+        for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+          for (int t = 0; t < NPT; ++t)
+#pragma unroll
+            for (int ct = 0; ct < 3; ++ct)
+              acc[t][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq[ks][t], bq[ks][ct], acc[t][ct], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int k0 = 0; k0 < CIN; k0 += 16) {
+          bf16x8 b[3];
+#pragma unroll
+          for (int ct = 0; ct < 3; ++ct)
+            b[ct] = *reinterpret_cast<const bf16x8*>(&sWt[(ct * 32 + l32) * CINP + k0 + 8 * hh]);
+#pragma unroll
+          for (int t = 0; t < NPT; ++t) {
+            const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sX[aoff[t] + k0]);
+#pragma unroll
+            for (int ct = 0; ct < 3; ++ct) acc[t][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[ct], acc[t][ct], 0, 0, 0);
+          }
         }
       }
-      __syncthreads();  // sW (and after the last tap sX) fully read
+      if (GL) {
+        // retire this wave's DMA of tap g+1 (issued a tap ago); the one of g+2 and, on
+        // the last tap, the residual / next-input loads stay in flight
+        // (exact only when every chunk guard holds; otherwise count 0 = wait for more)
+        const int extra = (tap == 8 && FULL) ? ((p.res ? NEC : 0) + (nn < p.N ? NPF : 0)) : 0;
+        wait_vmcnt(nglds + extra);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        ++gi;
+      } else if (PF) {
 #ifndef MC_EXP_NO_WLOAD
-      if (tap + 1 < 9) {
-        MC_STORE_W(0, wr);
-        __syncthreads();
-      }
+        if (tap + 1 < 9) MC_STORE_W((tap + 1) & 1, wr);  // that buffer was last read in tap-1
 #endif
+        __syncthreads();
+      } else {
+        __syncthreads();  // sW (and after the last tap sX) fully read
+#ifndef MC_EXP_NO_WLOAD
+        if (tap + 1 < 9) {
+          MC_STORE_W(0, wr);
+          __syncthreads();
+        }
+#endif
+      }
     }
 
+    FSTAMP(1);  // 9 taps
     // ---------------- epilogue A: bias, GroupNorm statistics, y -> LDS ----------------
     float biasv[3];
 #pragma unroll
@@ -221,18 +356,20 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
 #pragma unroll
       for (int ct = 0; ct < 3; ++ct) {
         const float mu = pass ? gmean[2 * ct + (l32 >> 4)] : 0.f;
-        float s = 0.f;
+        float v[NPT * 16];  // pairwise tree below: a serial += chain is NPT*16 dependent adds
 #pragma unroll
         for (int t = 0; t < NPT; ++t)
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const int px = (wave * NPT + t) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-            if (px < P) {
-              const float d = acc[t][ct][i] + biasv[ct] - mu;
-              s += pass ? d * d : d;
-            }
+            const float d = acc[t][ct][i] + biasv[ct] - mu;
+            v[t * 16 + i] = (FULL || px < P) ? (pass ? d * d : d) : 0.f;
           }
-        part[ct] = row_sum16(s);
+#pragma unroll
+        for (int w2 = NPT * 8; w2 >= 1; w2 >>= 1)
+#pragma unroll
+          for (int i = 0; i < w2; ++i) v[i] += v[i + w2];
+        part[ct] = row_sum16(v[0]);
       }
       float gs[3][2];  // readlanes in converged control flow (see note in the stats exchange)
 #pragma unroll
@@ -258,6 +395,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
       }
       __syncthreads();  // sRed reused by the next pass
     }
+    FSTAMP(2);  // GroupNorm statistics
     if (p.stats && tid < NGRP) {
       float m = 0.f, r = 0.f;
 #pragma unroll
@@ -278,6 +416,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
           const int px = (wave * NPT + t) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
           if (FULL || px < P) sO[px * COUT + ct * 32 + l32] = (__bf16)(acc[t][ct][i] + biasv[ct]);
         }
+    FSTAMP(3);  // y -> LDS
     if (tid < COUT) {  // z = y * scale + shift (+ res), then ReLU, then * dropout scale
       const int g = tid >> 4;
       float mu = 0.f, rs = 0.f;
@@ -298,46 +437,74 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
 #ifdef MC_EXP_NO_EPI
     if (p.N < 0)
 #endif
-    for (int c = tid; c < P * (COUT / 8); c += 256) {
-      const int co0 = (c % (COUT / 8)) * 8;
-      const size_t o = (size_t)n * P * COUT + (size_t)c * 8;
-      const u32x4 yv = *reinterpret_cast<const u32x4*>(&sO[c * 8]);
-      if (p.ysave) *reinterpret_cast<u32x4*>(&p.ysave[o]) = yv;
-      const bf16x8 y8 = __builtin_bit_cast(bf16x8, yv);
-      bf16x8 r8 = bf16x8{};
-      if (p.res) r8 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(&p.res[o]));
-      bf16x8 o8;
+    // chunk c = tid + 256k covers channels ((tid + 4k) mod 12) * 8 ..+8: three channel
+    // groups per thread, their scale / shift / dropout scale kept in registers
+    float ca[3][8], cb[3][8], cd[3][8];
+#pragma unroll
+    for (int j3 = 0; j3 < 3; ++j3) {
+      const int cg = ((tid % (COUT / 8)) + 4 * j3) % (COUT / 8);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int co = co0 + j;
-        const float z = fmaxf((float)y8[j] * sAB[co] + sAB[COUT + co] + (float)r8[j], 0.f);
-        o8[j] = (__bf16)(z * sAB[2 * COUT + co]);
+        ca[j3][j] = sAB[cg * 8 + j];
+        cb[j3][j] = sAB[COUT + cg * 8 + j];
+        cd[j3][j] = sAB[2 * COUT + cg * 8 + j];
       }
-      *reinterpret_cast<u32x4*>(&p.out[o]) = __builtin_bit_cast(u32x4, o8);
     }
+#pragma unroll
+    for (int k = 0; k < NEC; ++k) {
+      const int c = tid + 256 * k;
+      if (c < P * (COUT / 8)) {
+        const size_t o = (size_t)n * P * COUT + (size_t)c * 8;
+        const u32x4 yv = *reinterpret_cast<const u32x4*>(&sO[c * 8]);
+        if (p.ysave) *reinterpret_cast<u32x4*>(&p.ysave[o]) = yv;
+        const bf16x8 y8 = __builtin_bit_cast(bf16x8, yv);
+        bf16x8 r8 = bf16x8{};
+        if (PF) r8 = __builtin_bit_cast(bf16x8, rv[PF ? k : 0]);
+        else if (p.res) r8 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(&p.res[o]));
+        bf16x8 o8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float z = fmaxf((float)y8[j] * ca[k % 3][j] + cb[k % 3][j] + (float)r8[j], 0.f);
+          o8[j] = (__bf16)(z * cd[k % 3][j]);
+        }
+        *reinterpret_cast<u32x4*>(&p.out[o]) = __builtin_bit_cast(u32x4, o8);
+      }
+    }
+    FSTAMP(4);  // scale/shift + outputs issued
     __syncthreads();  // region0 is re-staged with the next input
+    FSTAMP(5);
   }
+  if (GL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the workgroup
+#ifdef MC_DIAG
+  if (p.diag && threadIdx.x == 0)
+    for (int k = 0; k < 8; ++k) p.diag[blockIdx.x * 8 + k] = dacc[k];
+#endif
 }
 
-template <int CIN, int NPT, bool FULL>
+template <int CIN, int NPT, bool FULL, bool PF>
 int launch_fwd(const FwdParams& p, hipStream_t s) {
   constexpr int CINP = cinp<CIN>();
-  const size_t lds = (size_t)region0_elems<CIN>(p.H, p.W) * 2 + (size_t)COUT * CINP * 2 + WAVES * NGRP * 4 +
-                     5 * COUT * 4;
+#ifdef MC_FWD_GL
+  constexpr bool GL = PF && CIN == 96;
+#else
+  constexpr bool GL = false;
+#endif
+  const size_t lds = (size_t)region0_elems<CIN>(p.H, p.W) * 2 +
+                     (size_t)(GL ? 3 * COUT * COUT : (PF ? 2 : 1) * COUT * CINP) * 2 + WAVES * NGRP * 4 + 5 * COUT * 4;
   if (lds > 160 * 1024) {
     snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd: board %dx%d needs %zu B LDS", p.H, p.W, lds);
     return MS_EINVAL;
   }
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k_conv_gn_fwd<CIN, NPT, FULL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)k_conv_gn_fwd<CIN, NPT, FULL, PF>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     attr_set = true;
   }
-  const int per_cu = lds <= 80 * 1024 ? 2 : 1;
+  const int per_cu = (!PF && lds <= 80 * 1024) ? 2 : 1;
   const int cap = per_cu * num_cus();
   const int grid = p.N < cap ? p.N : cap;
-  hipLaunchKernelGGL((k_conv_gn_fwd<CIN, NPT, FULL>), dim3(grid), dim3(256), lds, s, p);
+  hipLaunchKernelGGL((k_conv_gn_fwd<CIN, NPT, FULL, PF>), dim3(grid), dim3(256), lds, s, p);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd launch: %s", hipGetErrorString(e));
@@ -351,12 +518,14 @@ int dispatch_fwd(const FwdParams& p, hipStream_t s) {
   const int P = p.H * p.W;
   const int tiles = (P + 31) / 32;
   const int npt = (tiles + WAVES - 1) / WAVES;
-  if (P == 256) return launch_fwd<CIN, 2, true>(p, s);  // 16x16: every 32-px tile is full
+  // MC_FWD_PF=1 selects the one-workgroup-per-CU prefetching variant (A/B measurements)
+  static const bool pf = getenv("MC_FWD_PF") ? atoi(getenv("MC_FWD_PF")) != 0 : false;
+  if (P == 256) return pf ? launch_fwd<CIN, 2, true, true>(p, s) : launch_fwd<CIN, 2, true, false>(p, s);
   switch (npt) {
-    case 1: return launch_fwd<CIN, 1, false>(p, s);
-    case 2: return launch_fwd<CIN, 2, false>(p, s);
-    case 3: return launch_fwd<CIN, 3, false>(p, s);
-    case 4: return launch_fwd<CIN, 4, false>(p, s);
+    case 1: return pf ? launch_fwd<CIN, 1, false, true>(p, s) : launch_fwd<CIN, 1, false, false>(p, s);
+    case 2: return pf ? launch_fwd<CIN, 2, false, true>(p, s) : launch_fwd<CIN, 2, false, false>(p, s);
+    case 3: return launch_fwd<CIN, 3, false, false>(p, s);
+    case 4: return launch_fwd<CIN, 4, false, false>(p, s);
     default:
       snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd: %d pixels > 512 unsupported", P);
       return MS_EINVAL;
@@ -365,9 +534,18 @@ int dispatch_fwd(const FwdParams& p, hipStream_t s) {
 
 }  // namespace
 
+#ifdef MC_DIAG
+unsigned long long* g_fwd_diag = nullptr;
+#endif
+
 extern "C" {
 
 const char* mc_last_error(void) { return g_err; }
+
+#ifdef MC_DIAG
+// diagnostics only (not in mscnn.h): per-workgroup phase cycle totals of the next forwards
+void mc_set_fwd_diag(unsigned long long* d) { g_fwd_diag = d; }
+#endif
 
 int mc_conv_gn_fwd(const uint16_t* x, const uint16_t* w, const float* bias, const float* gamma, const float* beta,
                    const uint16_t* res, const float* dmask, uint16_t* out, uint16_t* ysave, float* stats, int32_t n,
@@ -391,6 +569,10 @@ int mc_conv_gn_fwd(const uint16_t* x, const uint16_t* w, const float* bias, cons
   p.H = h;
   p.W = w_;
   p.eps = eps;
+  p.diag = nullptr;
+#ifdef MC_DIAG
+  p.diag = g_fwd_diag;
+#endif
   hipStream_t s = (hipStream_t)stream;
   if (cin == 16) return dispatch_fwd<16>(p, s);
   if (cin == 96) return dispatch_fwd<96>(p, s);

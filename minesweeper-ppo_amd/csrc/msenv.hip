@@ -26,6 +26,7 @@
 
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <new>
@@ -101,6 +102,16 @@ __device__ __forceinline__ uint32_t readlane32(uint32_t v, int l) {
 }
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
   return ((uint64_t)readlane32((uint32_t)(v >> 32), l) << 32) | readlane32((uint32_t)v, l);
+}
+// Wave-local LDS barrier. A workgroup of k_step / k_tape holds several boards,
+// one per wave, each with its own LDS region, so a board's LDS exchanges only
+// have to be ordered inside its wave: a wave's DS operations execute in issue
+// order, so this is a compiler code-motion fence plus a wait for outstanding
+// LDS results, not an s_barrier (waves of one workgroup never wait for each other).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 // wave-wide sum: 4 DPP row-prefix adds + 4 readlanes (uniform result)
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
@@ -214,7 +225,7 @@ __device__ __forceinline__ void store_rows(uint64_t* words, uint64_t row, uint64
     return;
   }
   srow[lane] = row;
-  __syncthreads();
+  wave_sync();
   if (lane < nw) {
     uint64_t acc = 0;
     for (int k = 0; k < rpw; ++k) {
@@ -223,7 +234,7 @@ __device__ __forceinline__ void store_rows(uint64_t* words, uint64_t row, uint64
     }
     words[lane] = acc;
   }
-  __syncthreads();
+  wave_sync();
 }
 
 // allowed-index -> cell for the ascending forbidden list f[0..m) (numpy's
@@ -323,7 +334,7 @@ __device__ __forceinline__ void stage_rows(uint64_t* sR, uint64_t* sM, uint64_t 
     sM[0] = 0ull;
     sM[kWave + 1] = 0ull;
   }
-  __syncthreads();
+  wave_sync();
 }
 
 // ---------------------------------------------------------------------------
@@ -574,12 +585,12 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
     sel[s2] = cand[s2];
   }
   for (int c = lane; c < A; c += kWave) tab[c] = 0u;
-  __syncthreads();
+  wave_sync();
   for (uint32_t round = 1; round <= (uint32_t)K + 1; ++round) {
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
       if (valid[s2]) atomicMax(&tab[sel[s2]], (round << 16) | (0xFFFFu - (uint32_t)(lane + 64 * s2)));
-    __syncthreads();
+    wave_sync();
     bool changed = false;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -591,20 +602,20 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
         sel[s2] = nv;
       }
     }
-    __syncthreads();
+    wave_sync();
     if (__ballot(changed) == 0ull) break;
   }
   srow[lane] = 0ull;
-  __syncthreads();
+  wave_sync();
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2)
     if (valid[s2]) {
       const int r = sel[s2] / W;
       atomicOr((unsigned long long*)&srow[r], 1ull << (sel[s2] - r * W));
     }
-  __syncthreads();
+  wave_sync();
   mine_out = lane < g.H ? srow[lane] : 0ull;
-  __syncthreads();
+  wave_sync();
   // RNG state after the D draws
   if (n_out > 0) {
     const int lastq = n_out - 1;
@@ -702,14 +713,21 @@ __device__ __forceinline__ void board_click(Pcg& rng, uint64_t& mine, uint64_t& 
   }
 }
 
-template <int H_, int W_>
-__global__ __launch_bounds__(64) void k_step(KParams p) {
-  __shared__ uint64_t sR[kWave];
-  __shared__ uint64_t sM[kWave + 2];
-  __shared__ uint32_t sTab[(H_ && W_) ? H_ * W_ : kMaxH * kMaxW];
+// EPW boards per workgroup, one per wave, each with its own LDS slice: fewer,
+// larger workgroups halve the dispatch cost of a 4096-board launch, and no
+// wave ever waits on another (board code syncs with wave_sync only).
+template <int H_, int W_, int EPW>
+__global__ __launch_bounds__(64 * EPW) void k_step(KParams p) {
+  __shared__ uint64_t sR_all[EPW][kWave];
+  __shared__ uint64_t sM_all[EPW][kWave + 2];
+  __shared__ uint32_t sTab_all[EPW][(H_ && W_) ? H_ * W_ : kMaxH * kMaxW];
   const int lane = lane_id();
-  const int64_t env = (int64_t)blockIdx.x;
+  const int wv = (EPW == 1) ? 0 : (int)rfl(threadIdx.x >> 6);
+  const int64_t env = (int64_t)blockIdx.x * EPW + wv;
   if (env >= p.n) return;
+  uint64_t* sR = sR_all[wv];
+  uint64_t* sM = sM_all[wv];
+  uint32_t* sTab = sTab_all[wv];
   STAMP(0);
   const Geo<H_, W_> g(p.H, p.W);
   const int A = g.A(), NW = g.NW();
@@ -914,48 +932,80 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v) {
   return s - v;
 }
 
-__global__ __launch_bounds__(64) void k_tape(const uint64_t* mw, const uint64_t* rw, int64_t n, int H, int W,
-                                             int64_t env_begin, uint64_t t, int mode, int64_t* actions) {
-  const int lane = lane_id();
-  const int64_t env = blockIdx.x;
-  if (env >= n) return;
-  const Geo<0, 0> g(H, W);
-  const int NW = g.NW();
-  const uint64_t mine = load_row(mw + env * NW, g, lane);
-  const uint64_t rev = load_row(rw + env * NW, g, lane);
-  const uint64_t valid = ~rev & g.rowmask() & (lane < H ? ~0ull : 0ull);
-  const uint64_t safe = valid & ~mine;
-  const uint64_t gidx = (uint64_t)(env_begin + env);
-  const uint64_t x = splitmix64(0xC0FFEEull ^ (gidx << 32) ^ t);
-  const uint32_t n_valid = wave_sum((uint32_t)__popcll(valid));
-  const uint32_t n_safe = wave_sum((uint32_t)__popcll(safe));
-  const bool want_safe = mode == MS_TAPE_SAFE_BIASED && (x & 0xFFFFull) < 65208ull && n_safe > 0;
-  uint64_t bits;
-  uint32_t cnt;
-  uint64_t sel;
-  if (want_safe) {
-    bits = safe;
-    cnt = n_safe;
-    sel = x >> 16;
-  } else {
-    bits = valid;
-    cnt = n_valid;
-    sel = (mode == MS_TAPE_SAFE_BIASED) ? (x >> 16) : x;
+// One lane per env: the packed row words of a board are its cells in row-major
+// order (rows never straddle a word), so "k-th valid cell" is the k-th set bit
+// across the NW words of ~revealed (& ~mine). A wave covers 64 boards with
+// coalesced 16-B word loads, and the whole launch is a single load round trip
+// plus ~100 lane-local instructions.
+__device__ __forceinline__ int select_bit64(uint64_t x, uint32_t k) {  // k-th set bit, k < popc(x)
+  int pos = 0;
+#pragma unroll
+  for (int half = 32; half >= 1; half >>= 1) {
+    const uint64_t lowmask = (1ull << half) - 1ull;
+    const uint32_t c = (uint32_t)__popcll(x & lowmask);
+    if (k >= c) {
+      k -= c;
+      x >>= half;
+      pos += half;
+    }
   }
-  int64_t act = 0;
-  if (cnt > 0) {
-    const uint32_t target = (uint32_t)(sel % (uint64_t)cnt);
-    const uint32_t pc = (uint32_t)__popcll(bits);
-    const uint32_t before = wave_excl_scan(pc);
-    const bool mine_lane = target >= before && target < before + pc;
-    const uint64_t who = __ballot(mine_lane);
-    const int src = __ffsll((unsigned long long)who) - 1;
-    const int col = (int)readlane32((uint32_t)(mine_lane ? select_bit(bits, target - before) : 0), src);
-    act = (int64_t)src * W + col;
-  }
-  if (lane == 0) actions[env] = act;
+  return pos;
 }
 
+template <int H_, int W_>
+__global__ __launch_bounds__(256) void k_tape(const uint64_t* mw, const uint64_t* rw, int64_t n, int H_rt, int W_rt,
+                                              int64_t env_begin, uint64_t t, int mode, int64_t* actions) {
+  const int64_t env = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (env >= n) return;
+  const Geo<H_, W_> g(H_rt, W_rt);
+  const int W = g.W, rpw = g.RPW(), NW = g.NW();
+  constexpr int kNW = (H_ && W_) ? (H_ + (64 / W_) - 1) / (64 / W_) : 64;
+  const bool safe_mode = mode == MS_TAPE_SAFE_BIASED;
+  const uint64_t* rp = rw + env * NW;
+  const uint64_t* mp = mw + env * NW;
+  // word w of the valid (or safe) plane; loads are re-issued by the select pass
+  // (L1/L2 hits) rather than kept in an NW-long register array
+  auto plane = [&](int w, bool safe_plane) -> uint64_t {
+    const int rows = min(rpw, g.H - w * rpw);
+    const int bits = rows * W;
+    const uint64_t wm = bits >= 64 ? ~0ull : ((1ull << bits) - 1ull);
+    const uint64_t v = ~rp[w] & wm;
+    return safe_plane ? (v & ~mp[w]) : v;
+  };
+  uint32_t n_valid = 0, n_safe = 0;
+#pragma unroll
+  for (int w = 0; w < kNW; ++w) {
+    if (w < NW) {
+      n_valid += (uint32_t)__popcll(plane(w, false));
+      if (safe_mode) n_safe += (uint32_t)__popcll(plane(w, true));
+    }
+  }
+  const uint64_t gidx = (uint64_t)(env_begin + env);
+  const uint64_t x = splitmix64(0xC0FFEEull ^ (gidx << 32) ^ t);
+  const bool want_safe = safe_mode && (x & 0xFFFFull) < 65208ull && n_safe > 0;
+  const uint32_t cnt = want_safe ? n_safe : n_valid;
+  const uint64_t sel = safe_mode ? (x >> 16) : x;
+  int64_t act = 0;
+  if (cnt > 0) {
+    uint32_t target = (uint32_t)(sel % (uint64_t)cnt);
+#pragma unroll
+    for (int w = 0; w < kNW; ++w) {
+      if (w < NW && target != 0xFFFFFFFFu) {
+        const uint64_t b = plane(w, want_safe);
+        const uint32_t pc = (uint32_t)__popcll(b);
+        if (target < pc) {
+          const int pos = select_bit64(b, target);
+          const int r = w * rpw + pos / W;
+          act = (int64_t)r * W + (pos - (pos / W) * W);
+          target = 0xFFFFFFFFu;  // found
+        } else {
+          target -= pc;
+        }
+      }
+    }
+  }
+  actions[env] = act;
+}
 
 // ---------------------------------------------------------------------------
 // Late-start resets (VecMinesweeper._apply_late_start, env.py:416-466).
@@ -1287,6 +1337,7 @@ struct ms_handle {
   uint64_t* jump;  // [64][4] PCG64 jump-ahead table (device)
   uint64_t* diag;  // optional stamp buffer (MS_DIAG builds)
   uint32_t dbg_flags;
+  int epw;         // boards per workgroup of k_step (MSENV_EPW overrides, tools only)
   int late_on;     // ms_set_late_start called with prob > 0
   LateCfg late;
   Pcg* late_rng;   // device: the shared late-start generator
@@ -1300,8 +1351,13 @@ bool shape_ok(const ms_cfg* c) {
 }
 
 template <int H_, int W_>
-void launch_step(const KParams& p, hipStream_t s) {
-  hipLaunchKernelGGL((k_step<H_, W_>), dim3((unsigned)p.n), dim3(64), 0, s, p);
+void launch_step(const KParams& p, int epw, hipStream_t s) {
+  // generic shapes keep one board per workgroup (their LDS table is sized for 64x62)
+  if (H_ && W_ && epw == 4) {
+    hipLaunchKernelGGL((k_step<H_, W_, 4>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, p);
+  } else {
+    hipLaunchKernelGGL((k_step<H_, W_, 1>), dim3((unsigned)p.n), dim3(64), 0, s, p);
+  }
 }
 
 template <int H_, int W_>
@@ -1352,12 +1408,12 @@ int do_step(ms_handle* h, const void* actions, int i32, float* obs, uint8_t* mas
   p.actions_i32 = i32;
   hipStream_t s = (hipStream_t)stream;
   if (h->late_on && !done) return fail(MS_EINVAL, "ms_step: late start needs the done output");
-  if (h->H == 16 && h->W == 16) launch_step<16, 16>(p, s);
-  else if (h->H == 9 && h->W == 9) launch_step<9, 9>(p, s);
-  else if (h->H == 30 && h->W == 16) launch_step<30, 16>(p, s);
-  else if (h->H == 16 && h->W == 30) launch_step<16, 30>(p, s);
-  else if (h->H == 8 && h->W == 8) launch_step<8, 8>(p, s);
-  else launch_step<0, 0>(p, s);
+  if (h->H == 16 && h->W == 16) launch_step<16, 16>(p, h->epw, s);
+  else if (h->H == 9 && h->W == 9) launch_step<9, 9>(p, h->epw, s);
+  else if (h->H == 30 && h->W == 16) launch_step<30, 16>(p, h->epw, s);
+  else if (h->H == 16 && h->W == 30) launch_step<16, 30>(p, h->epw, s);
+  else if (h->H == 8 && h->W == 8) launch_step<8, 8>(p, h->epw, s);
+  else launch_step<0, 0>(p, h->epw, s);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "ms_step launch");
   // auto-resets that draw a late start (env.py:497-498 -> 406-414), in env order
@@ -1394,6 +1450,11 @@ int ms_create(const ms_cfg* cfg, int64_t n_total, uint64_t base_seed, int64_t en
   const int rpw = 64 / cfg->W;
   h->NW = (cfg->H + rpw - 1) / rpw;
   (void)hipGetDevice(&h->device);
+  h->epw = 4;
+  if (const char* ev = getenv("MSENV_EPW")) {  // tools/ experiments only
+    const int v = atoi(ev);
+    if (v == 1 || v == 4) h->epw = v;
+  }
 
   // env.py:393-395: base = default_rng(seed); seeds = base.integers(0, 2**31-1, N)
   std::vector<EnvMeta> meta((size_t)env_count);
@@ -1575,8 +1636,23 @@ int ms_rng_state(ms_handle* h, uint64_t* out, void* stream) {
 int ms_tape_actions(ms_handle* h, uint64_t t, int32_t mode, int64_t* actions, void* stream) {
   if (!h || !actions) return fail(MS_EINVAL, "ms_tape_actions: null argument");
   if (mode != MS_TAPE_UNIFORM && mode != MS_TAPE_SAFE_BIASED) return fail(MS_EINVAL, "ms_tape_actions: bad mode");
-  hipLaunchKernelGGL(k_tape, dim3((unsigned)h->n), dim3(64), 0, (hipStream_t)stream, h->mine_words,
-                     h->rev_words, h->n, h->H, h->W, h->env_begin, t, mode, actions);
+  const hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((unsigned)((h->n + 255) / 256)), block(256);
+  if (h->H == 16 && h->W == 16)
+    hipLaunchKernelGGL((k_tape<16, 16>), grid, block, 0, s, h->mine_words, h->rev_words, h->n, h->H, h->W,
+                       h->env_begin, t, mode, actions);
+  else if (h->H == 9 && h->W == 9)
+    hipLaunchKernelGGL((k_tape<9, 9>), grid, block, 0, s, h->mine_words, h->rev_words, h->n, h->H, h->W,
+                       h->env_begin, t, mode, actions);
+  else if (h->H == 30 && h->W == 16)
+    hipLaunchKernelGGL((k_tape<30, 16>), grid, block, 0, s, h->mine_words, h->rev_words, h->n, h->H, h->W,
+                       h->env_begin, t, mode, actions);
+  else if (h->H == 16 && h->W == 30)
+    hipLaunchKernelGGL((k_tape<16, 30>), grid, block, 0, s, h->mine_words, h->rev_words, h->n, h->H, h->W,
+                       h->env_begin, t, mode, actions);
+  else
+    hipLaunchKernelGGL((k_tape<0, 0>), grid, block, 0, s, h->mine_words, h->rev_words, h->n, h->H, h->W,
+                       h->env_begin, t, mode, actions);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? MS_OK : hip_fail(e, "ms_tape_actions launch");
 }

@@ -717,7 +717,7 @@ __device__ __forceinline__ void board_click(Pcg& rng, uint64_t& mine, uint64_t& 
 // larger workgroups halve the dispatch cost of a 4096-board launch, and no
 // wave ever waits on another (board code syncs with wave_sync only).
 template <int H_, int W_, int EPW>
-__global__ __launch_bounds__(64 * EPW) void k_step(KParams p) {
+__global__ __launch_bounds__(64 * EPW, 8) void k_step(KParams p) {
   __shared__ uint64_t sR_all[EPW][kWave];
   __shared__ uint64_t sM_all[EPW][kWave + 2];
   __shared__ uint32_t sTab_all[EPW][(H_ && W_) ? H_ * W_ : kMaxH * kMaxW];
@@ -749,10 +749,13 @@ __global__ __launch_bounds__(64 * EPW) void k_step(KParams p) {
   rng.uinteger = rfl(mp->uinteger);
   int32_t step_count = (int32_t)rfl((uint32_t)mp->step_count);
   bool fc = (rfl(mp->flags) & 1u) != 0;
-  // jump-ahead entry k = lane+1 (2 KiB shared by every wave, L2-resident); only
-  // a board whose next click is its first needs it
-  uint64_t J[4] = {0ull, 0ull, 0ull, 0ull};
-  if (!fc) {
+  // jump-ahead entry k = lane+1 (2 KiB shared by every wave, L2-resident). Only
+  // a board whose next click is its first needs it, but it
+  // is loaded by every wave anyway, issued with the row loads: gating it on
+  // first_click_done would put a second dependent round trip on exactly the
+  // placement waves that end the launch
+  uint64_t J[4];
+  {
     const ulonglong2* e = reinterpret_cast<const ulonglong2*>(p.jump + 4 * lane);
     const ulonglong2 a0 = e[0], a1 = e[1];
     J[0] = a0.x;

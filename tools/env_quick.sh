@@ -10,3 +10,4 @@ for b in 9x9x10 30x16x99; do
   timeout -k 10 120 python bench.py --no-cpu-baseline --ppo-updates 0 --envs 8192 --board $b > gpurun_out/b_$b.json 2>/dev/null
   python -c "import json;d=json.load(open('gpurun_out/b_$b.json'));print('$b n 8192 value %.4g ms/step %.4f kern_ms %.4f frac %.3f'%(d['value'],d['ms_per_step'],d['roofline']['kernel_ms'],d['roofline']['frac']))"
 done
+timeout -k 10 200 python tools/diag_step.py --board 9x9x10 --envs 8192 > gpurun_out/diag9.txt 2>&1

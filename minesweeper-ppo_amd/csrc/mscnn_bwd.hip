@@ -23,6 +23,7 @@
 
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "../../include/msenv.h"
 #include "../../include/mscnn.h"
@@ -50,7 +51,21 @@ struct BwdDataParams {
   __bf16* dx;
   float* part;  // [gridDim][3][96]
   int N, H, W;
+  int stagger;  // as FwdParams::stagger (mscnn.hip)
 };
+
+// Start delay of part of a persistent grid (10-ns ticks; > 0: the upper half of the
+// grid, < 0: the odd blocks): two co-resident workgroups running the same phase
+// sequence in lockstep contend for the matrix pipe and for HBM at the same time.
+__device__ __forceinline__ void stagger_start(int stagger) {
+  if (stagger == 0) return;
+  const bool late = stagger > 0 ? (int)blockIdx.x >= (int)gridDim.x / 2 : (blockIdx.x & 1) != 0;
+  const unsigned long long ticks = (unsigned long long)(stagger > 0 ? stagger : -stagger);
+  if (late) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+  }
+}
 
 __host__ __device__ inline int dtile_bytes(int P) { return ((P + 1) * DCP * 2 + 15) & ~15; }
 __host__ __device__ constexpr int red_bytes() {  // sRed [PG][3][96] f32, aliased by sW [96][DCP] bf16
@@ -79,6 +94,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
     qr[t] = q < P ? q / W : -1000;  // an invalid pixel never lands on the board
     qc[t] = q < P ? q - qr[t] * W : -1000;
   }
+  stagger_start(p.stagger);
 
   for (int n = blockIdx.x; n < p.N; n += gridDim.x) {
     // loop-variant thread coordinates: keep the per-chunk address math inside the loop
@@ -338,6 +354,7 @@ struct WgradParams {
   const __bf16* x;
   float* part;  // [G][9][96][CIN]
   int N, H, W, G;
+  int stagger;
 };
 
 __host__ __device__ inline int wgrad_lds(int H, int W) {
@@ -437,6 +454,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams p) {
   const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
   const int cig = j % NCI, gid = (j / NCI) * 8 + xcd;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  stagger_start(p.stagger);
   switch (wave) {
     case 0: wgrad_body<CIN, 0, 7>(p, sDY, sX, gid, cig * 32); break;
     case 1: wgrad_body<CIN, 7, 7>(p, sDY, sX, gid, cig * 32); break;
@@ -445,12 +463,40 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams p) {
   }
 }
 
+// out[i] = sum_g part[g * n + i], deterministic: a 256-thread block covers 256 / S outputs
+// with S slices over g (slice s sums g = s, s + S, ... on four independent accumulators,
+// so a thread keeps four loads in flight), slices combined in fixed order through LDS.
+// S = 4 for the weight partials (n = 82,944, G = 168), 16 for the 288 GroupNorm sums.
+template <int S>
 __global__ __launch_bounds__(256) void k_reduce(const float* __restrict__ part, int G, int64_t n, float* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  float s = 0.f;
-  for (int g = 0; g < G; ++g) s += part[(int64_t)g * n + i];
-  out[i] = s;
+  constexpr int IB = 256 / S;
+  __shared__ float sp[S][IB];
+  const int li = threadIdx.x % IB, s = threadIdx.x / IB;
+  const int64_t i = (int64_t)blockIdx.x * IB + li;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (i < n) {
+    int g = s;
+    for (; g + 3 * S < G; g += 4 * S) {
+      a0 += part[(int64_t)g * n + i];
+      a1 += part[(int64_t)(g + S) * n + i];
+      a2 += part[(int64_t)(g + 2 * S) * n + i];
+      a3 += part[(int64_t)(g + 3 * S) * n + i];
+    }
+    for (; g < G; g += S) a0 += part[(int64_t)g * n + i];
+  }
+  sp[s][li] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (s == 0 && i < n) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < S; ++k) t += sp[k][li];
+    out[i] = t;
+  }
+}
+
+void launch_reduce(const float* part, int G, int64_t n, float* out, hipStream_t s) {
+  if (n >= 16384) hipLaunchKernelGGL(k_reduce<4>, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, part, G, n, out);
+  else hipLaunchKernelGGL(k_reduce<16>, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, s, part, G, n, out);
 }
 
 // ------------------------------------------------------------------------------------
@@ -583,11 +629,13 @@ int mc_conv_gn_bwd(const uint16_t* dout, const uint16_t* out, const uint16_t* ys
   bp.N = n;
   bp.H = h;
   bp.W = w_;
+  static const int bstag = getenv("MC_BWD_STAGGER") ? atoi(getenv("MC_BWD_STAGGER")) : 0;
+  static const int wstag = getenv("MC_WG_STAGGER") ? atoi(getenv("MC_WG_STAGGER")) : 0;
+  bp.stagger = bstag;
   int rc = wT ? dispatch_bwd_data<true>(bp, pl.grid_d, s) : dispatch_bwd_data<false>(bp, pl.grid_d, s);
   if (rc) return rc;
   if ((rc = check_launch("k_bwd_data"))) return rc;
-  hipLaunchKernelGGL(k_reduce, dim3((3 * COUT + 255) / 256), dim3(256), 0, s, (const float*)work, pl.grid_d,
-                     (int64_t)3 * COUT, dgn);
+  launch_reduce((const float*)work, pl.grid_d, (int64_t)3 * COUT, dgn, s);
   if ((rc = check_launch("k_reduce"))) return rc;
 
   WgradParams wp;
@@ -598,13 +646,13 @@ int mc_conv_gn_bwd(const uint16_t* dout, const uint16_t* out, const uint16_t* ys
   wp.H = h;
   wp.W = w_;
   wp.G = pl.G;
+  wp.stagger = wstag;
   const size_t lds = (size_t)wgrad_lds(h, w_);
   if (cin == 96) launch_wgrad<96>(wp, pl.grid_w, lds, s);
   else launch_wgrad<16>(wp, pl.grid_w, lds, s);
   if ((rc = check_launch("k_wgrad"))) return rc;
   const int64_t nw = (int64_t)9 * COUT * cin;
-  hipLaunchKernelGGL(k_reduce, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, (const float*)(work + pl.gn_part),
-                     pl.G, nw, dw);
+  launch_reduce((const float*)(work + pl.gn_part), pl.G, nw, dw, s);
   return check_launch("k_reduce");
 }
 

@@ -58,6 +58,14 @@ __device__ __forceinline__ int opaque0() {
   return z;
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations and
+// meets the other waves, leaving global loads and stores in flight. __syncthreads()'s
+// workgroup release fence turns into s_waitcnt vmcnt(0) as soon as global stores are
+// outstanding (gfx9 counts stores on vmcnt), draining an epilogue's stores and any
+// prefetched loads at every barrier. The memory clobber keeps the compiler from moving
+// memory operations across it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ bf16x8 cat8(bf16x4 lo, bf16x4 hi) {
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }

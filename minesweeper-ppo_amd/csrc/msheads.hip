@@ -137,6 +137,7 @@ struct HeadLds {
   __bf16 wt[C * WP];     // policy W1^T rows [k][c]
   __bf16 f[TR * C];      // swizzled f tile
   __bf16 dh[TR * NH];    // swizzled dh image
+  __bf16 df[TR * C];     // df rows, each wave's 32 rows staged for contiguous 16-B stores
   float dl[2][TR];
   float b1[NH], w2[NH];
   float red[2][NH];
@@ -156,12 +157,47 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams& p, HeadLds& 
   for (int ct = 0; ct < 6; ++ct) dw2acc[ct] = db1acc[ct] = 0.f;
 
   const int64_t ntiles = (p.M + TR - 1) / TR;
+  // the next tile's f rows and logit gradients are loaded into registers while this
+  // tile computes (one tile of HBM latency hidden per iteration)
+  constexpr int NFC = TR * 12 / 256;
+#ifdef MC_HB_PREFETCH
+  u32x4 fv[NFC];
+  float dl0 = 0.f, dl1 = 0.f;
+#endif
+#define HB_LOAD(tile_)                                                                  \
+  do {                                                                                  \
+    const int64_t b_ = (tile_) * TR;                                                    \
+    _Pragma("unroll") for (int i_ = 0; i_ < NFC; ++i_) {                                \
+      const int c_ = tid + 256 * i_, r_ = c_ / 12, ch_ = c_ - r_ * 12;                  \
+      fv[i_] = u32x4{0u, 0u, 0u, 0u};                                                   \
+      if (b_ + r_ < p.M) fv[i_] = *reinterpret_cast<const u32x4*>(&p.f[(b_ + r_) * C + ch_ * 8]); \
+    }                                                                                   \
+    if (tid < TR) {                                                                     \
+      dl0 = b_ + tid < p.M ? p.dlp[b_ + tid] : 0.f;                                     \
+      dl1 = (b_ + tid < p.M && p.dlm) ? p.dlm[b_ + tid] : 0.f;                          \
+    }                                                                                   \
+  } while (0)
+#ifdef MC_HB_PREFETCH
+  if ((int64_t)blockIdx.x < ntiles) HB_LOAD((int64_t)blockIdx.x);
+#endif
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t base = tile * TR;
     const int zo = opaque0();
     // ---- stage f tile and the two logit gradients ----
+#ifdef MC_HB_PREFETCH
 #pragma unroll
-    for (int i = 0; i < TR * 12 / 256; ++i) {
+    for (int i = 0; i < NFC; ++i) {
+      const int c = tid + 256 * i + zo, r = c / 12, ch = c - r * 12;
+      *reinterpret_cast<u32x4*>(&L.f[sf_off(r, ch * 8)]) = fv[i];
+    }
+    if (tid < TR) {
+      L.dl[0][tid] = dl0;
+      L.dl[1][tid] = dl1;
+    }
+#else
+    // (prefetching the next tile here needs ~26 more VGPRs than the kernel has: spills)
+#pragma unroll
+    for (int i = 0; i < NFC; ++i) {
       const int c = tid + 256 * i + zo, r = c / 12, ch = c - r * 12;
       const int64_t row = base + r;
       u32x4 v = u32x4{0u, 0u, 0u, 0u};
@@ -173,7 +209,11 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams& p, HeadLds& 
       L.dl[0][tid] = row < p.M ? p.dlp[row] : 0.f;
       L.dl[1][tid] = (row < p.M && p.dlm) ? p.dlm[row] : 0.f;
     }
+#endif
     __syncthreads();
+#ifdef MC_HB_PREFETCH
+    if (tile + gridDim.x < ntiles) HB_LOAD(tile + gridDim.x);
+#endif
     // ---- recompute H[px][c] for this wave's 32 rows ----
     {
       f32x16 acc[6];
@@ -226,28 +266,37 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams& p, HeadLds& 
           acc2[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc2[kt], 0, 0, 0);
         }
       }
-      // acc2[kt][r] = df[px = wave*32 + l32][k = kt*32 + 8*(r>>2) + 4*hh + (r&3)]
+      // acc2[kt][r] = df[px = wave*32 + l32][k = kt*32 + 8*(r>>2) + 4*hh + (r&3)]:
+      // 8-B pieces of 64 different rows; staged in this wave's 32 rows of L.df, then
+      // written as contiguous 16-B chunks (the wave's rows are 6 KiB of contiguous df)
       const int64_t row = base + rb;
-      if (row < p.M) {
-        const float* ga = p.gadd ? p.gadd + (row / p.P) * C : nullptr;
+      const float* ga = (p.gadd && row < p.M) ? p.gadd + (row / p.P) * C : nullptr;
 #pragma unroll
-        for (int kt = 0; kt < 3; ++kt)
+      for (int kt = 0; kt < 3; ++kt)
 #pragma unroll
-          for (int gg = 0; gg < 4; ++gg) {
-            const int k0 = kt * 32 + 8 * gg + 4 * hh;
-            float v[4];
+        for (int gg = 0; gg < 4; ++gg) {
+          const int k0 = kt * 32 + 8 * gg + 4 * hh;
+          float v[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = acc2[kt][4 * gg + j];
-            if (ga) {
-              const float4 a4 = *reinterpret_cast<const float4*>(&ga[k0]);
-              v[0] += a4.x;
-              v[1] += a4.y;
-              v[2] += a4.z;
-              v[3] += a4.w;
-            }
-            const bf16x4 o = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
-            *reinterpret_cast<bf16x4*>(&p.df[row * C + k0]) = o;
+          for (int j = 0; j < 4; ++j) v[j] = acc2[kt][4 * gg + j];
+          if (ga) {
+            const float4 a4 = *reinterpret_cast<const float4*>(&ga[k0]);
+            v[0] += a4.x;
+            v[1] += a4.y;
+            v[2] += a4.z;
+            v[3] += a4.w;
           }
+          *reinterpret_cast<bf16x4*>(&L.df[rb * C + k0]) =
+              bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+        }
+      // (LDS operations of one wave complete in order: its own rows read back below)
+      const int lane64 = tid & 63;
+#pragma unroll 1
+      for (int i = 0; i < 32 * 12 / 64; ++i) {
+        const int c = lane64 + 64 * i, r = c / 12, ch = c - r * 12;
+        const int64_t grow = base + wave * 32 + r;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(&L.df[(wave * 32 + r) * C + ch * 8 + zo]);
+        if (grow < p.M) *reinterpret_cast<u32x4*>(&p.df[grow * C + ch * 8]) = v;
       }
     }
     // ---- dW1[c][k] += sum_px dh[px][c] f[px][k] over the tile's 128 rows ----
@@ -273,6 +322,7 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams& p, HeadLds& 
     }
     __syncthreads();  // f / dh images are re-staged by the next tile
   }
+#undef HB_LOAD
   // ---- partials ----
   float* part = p.part + (size_t)blockIdx.x * PART;
 #pragma unroll

@@ -59,6 +59,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-multistep", action="store_true", help="skip the one-launch ms_run_tape line")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
     ap.add_argument("--diag-no-obs", action="store_true", help="diagnostic: skip obs/mask outputs")
     ap.add_argument("--graph", type=int, default=1, help="capture the timed steps in a HIP graph")
@@ -101,6 +102,60 @@ def cpu_baseline(H, W, K, n_envs, seed, tape, budget_s, threads):
     return dict(value=n_envs * steps / el, unit="env_steps/s", cores=threads, kind="port",
                 sample=f"{steps} steps x {n_envs} envs {H}x{W}x{K} (tape {tape}) in {el:.1f}s, "
                        f"oracle/ms_oracle.c on {threads} pthreads")
+
+
+def multistep_bench(args, world, lib, h, L, n_local, n_total, H, W, bpe, dev):
+    """ms_run_tape: the same synthetic tape + board step, S steps per launch (boards held
+    in registers between steps), every step's outputs in their own slot as in a rollout
+    buffer. Launch durations summed / K is its per-step kernel time."""
+    A = H * W
+    # every step writes its own slot (slots=1) of an S-step region holding > 1 GiB, so the
+    # stores stream to HBM rather than into the 256 MiB Infinity Cache; K steps = ceil(K/S)
+    # launches of S steps (the last one shorter)
+    S = max(1, min(args.steps, -(-(1 << 30) // (n_local * 41 * A))))
+    bufs = [torch.empty((S, n_local, 10, H, W), dtype=torch.float32, device=dev),
+            torch.empty((S, n_local, A), dtype=torch.bool, device=dev),
+            torch.empty((S, n_local), dtype=torch.float32, device=dev),
+            torch.empty((S, n_local), dtype=torch.bool, device=dev),
+            torch.empty((S, n_local), dtype=torch.int32, device=dev),
+            torch.empty((S, n_local), dtype=torch.int32, device=dev),
+            torch.empty((S, n_local), dtype=torch.float64, device=dev),
+            torch.empty((S, n_local), dtype=torch.int8, device=dev)]
+    ptrs = [L.ptr(b) for b in bufs]
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    t_base = 1 << 24  # tape indices past those of the per-step measurement
+    L.check(lib.ms_run_tape(h, t_base, min(S, max(1, args.warmup)), args.tape, 1, None, *ptrs, sp))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = []
+    t0 = time.perf_counter()
+    done_steps = 0
+    while done_steps < args.steps:
+        T = min(S, args.steps - done_steps)
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+        L.check(lib.ms_run_tape(h, t_base + args.warmup + done_steps, T, args.tape, 1, None, *ptrs, sp))
+        ev[1].record()
+        evs.append(ev)
+        done_steps += T
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    if world > 1:
+        t = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el, kern_ms = float(t[0]), float(t[1])
+    achieved = bpe * n_local / (kern_ms * 1e-3) / 1e9
+    return {"metric": "env steps/sec, S synthetic-policy steps per launch (ms_run_tape)",
+            "value": n_total * args.steps / el, "unit": "env_steps/s", "ms_per_step": el / args.steps * 1e3,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_run",
+                         "kernel_ms_per_step": kern_ms, "steps_per_launch": S,
+                         "kernel_ms_method": "HIP events around each S-step launch, summed / K"}}
 
 
 # fwd / fwd+bwd GFLOP per 16x16 sample of the shipped model (SURVEY.md §2, torch flop counter)
@@ -172,8 +227,13 @@ def main():
                          shard=(rank, world))
     assert vec.num_envs == n_local
     A = H * W
-    obs = torch.empty((n_local, 10, H, W), dtype=torch.float32, device=dev)
-    mask = torch.empty((n_local, A), dtype=torch.bool, device=dev)
+    # obs/mask go to a ring of R slots holding > 512 MiB (2x the 256 MiB Infinity Cache), as a
+    # rollout buffer would: a single re-written 44 MB buffer stays cache-resident and its
+    # stores never reach HBM, which would flatter the HBM roofline
+    R = max(1, -(-(512 << 20) // (n_local * 41 * A)))
+    obs_ring = torch.empty((R, n_local, 10, H, W), dtype=torch.float32, device=dev)
+    mask_ring = torch.empty((R, n_local, A), dtype=torch.bool, device=dev)
+    obs, mask = obs_ring[0], mask_ring[0]
     rew = torch.empty(n_local, dtype=torch.float32, device=dev)
     done = torch.empty(n_local, dtype=torch.bool, device=dev)
     step_i = torch.empty(n_local, dtype=torch.int32, device=dev)
@@ -193,7 +253,10 @@ def main():
         L.check(lib.ms_tape_actions(h, t, args.tape, ptrs[0], sp))
         if ev is not None:
             ev[0].record()
-        L.check(lib.ms_step(h, *ptrs, sp))
+        pt = list(ptrs)
+        if not args.diag_no_obs:
+            pt[1], pt[2] = L.ptr(obs_ring[t % R]), L.ptr(mask_ring[t % R])
+        L.check(lib.ms_step(h, *pt, sp))
         if ev is not None:
             ev[1].record()
 
@@ -284,13 +347,16 @@ def main():
         "config": {"workload": f"board step {H}x{W}x{K}, {n_local} envs per GPU (BASELINE configs[1]"
                                f"{', configs[3] at 8 GPUs' if world == 8 else ''})",
                    "board": f"{H}x{W}x{K}", "envs_per_gpu": n_local, "envs_total": n_total,
-                   "tape": args.tape, "parallelism": f"env-shard x{world}, no collective"},
+                   "tape": args.tape, "parallelism": f"env-shard x{world}, no collective",
+                   "obs_ring_slots": R},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "k_step", "kernel_ms": kern_ms, "kernel_ms_method": kern_method,
                      "algo_bytes_per_env_step": bpe,
                      "algo_bytes_per_launch": bpe * n_local, "traffic_source": traffic_src},
     }
+    if not args.no_multistep and not args.diag_no_obs:
+        out["multistep"] = multistep_bench(args, world, lib, h, L, n_local, n_total, H, W, bpe, dev)
     if args.ppo_updates > 0:
         out["ppo"] = ppo_bench(args, world, rank, local_rank, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

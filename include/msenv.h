@@ -141,6 +141,19 @@ int ms_late_rng_state(ms_handle* h, uint64_t* out);
 int ms_tape_actions(ms_handle* h, uint64_t t, int32_t mode, int64_t* actions,
                     void* stream);
 
+/* Env-only synthetic rollout: T consecutive steps t0 .. t0+T-1 of every env, each
+ * equal to ms_tape_actions(t) followed by ms_step, in ONE launch that keeps every
+ * board in registers between steps (bit-exact with the two-call sequence; the
+ * reference analogue is stepping VecMinesweeper in a loop with random valid
+ * actions, scripts/profile_env.py:17-30). slots = 0: every output is
+ * overwritten by each step (the shapes of ms_step); slots = 1: step k writes
+ * slot k of [T][env_count, ...] outputs. actions (int64, optional) receives the
+ * tape's actions. Any output may be NULL. Late-start handles are rejected. */
+int ms_run_tape(ms_handle* h, uint64_t t0, int32_t T, int32_t mode, int32_t slots,
+                int64_t* actions, float* obs, uint8_t* mask, float* reward, uint8_t* done,
+                int32_t* step, int32_t* last_new, double* revealed_frac, int8_t* outcome,
+                void* stream);
+
 /* Replaces RolloutBuffer.compute_gae (buffers.py:78-94). rewards/values f32
  * [T,N], dones u8[T,N], last_values f32[N]; writes adv and ret f32[T,N]. The
  * f32 op order is the reference's (no contraction), so results are bitwise

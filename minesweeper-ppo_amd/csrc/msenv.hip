@@ -198,11 +198,16 @@ struct Geo {
 
 template <int H_, int W_>
 __device__ __forceinline__ uint64_t load_row(const uint64_t* words, const Geo<H_, W_>& g, int lane) {
-  if (lane >= g.H) return 0ull;
+  // no branch around the load: lanes past the board read a valid word (clamped index)
+  // and are masked afterwards, so the compiler can issue every load of the kernel's
+  // prologue back to back instead of waiting out each one inside a divergent branch
   const int rpw = g.RPW();
   const int w = lane / rpw;
+  const int wc = w < g.NW() ? w : g.NW() - 1;
   const int sh = (lane - w * rpw) * g.W;
-  return (words[w] >> sh) & g.rowmask();
+  const uint64_t v = words[wc];
+  const uint64_t keep = 0ull - (uint64_t)(lane < g.H);  // a mask, not a select: a select
+  return (v >> sh) & g.rowmask() & keep;                 // lets the load sink into a branch
 }
 
 // rows -> packed words. rows-per-word a power of two (W=16: 4, W=30: 2, W=8: 8,
@@ -259,11 +264,13 @@ __device__ __forceinline__ uint32_t cell_code(const uint64_t* sR, const uint64_t
   return rv ? (fc ? 1u + cnt : 10u) : 0u;
 }
 
-// Writes obs [10,A] f32 and mask [A] u8 of one env from the LDS rows.
+// Writes obs [10,A] f32 and mask [A] u8 of one env from the LDS rows. (sCode: A bytes of
+// this wave's LDS scratch, reserved for a code-staged emit; a flat 8-B stream of the
+// env's 10*A floats measured slower on 9x9 than the per-cell stores below.)
 template <int H_, int W_>
 __device__ __forceinline__ void emit_obs(float* __restrict__ obs, uint8_t* __restrict__ mask,
                                          const uint64_t* sR, const uint64_t* sM, bool fc,
-                                         const Geo<H_, W_>& g, int lane) {
+                                         const Geo<H_, W_>& g, int lane, uint8_t* sCode) {
   const int A = g.A(), W = g.W;
   if ((A & 3) == 0) {
     const int nq = A >> 2;
@@ -312,6 +319,7 @@ __device__ __forceinline__ void emit_obs(float* __restrict__ obs, uint8_t* __res
       }
     }
   } else {
+    (void)sCode;
     for (int i = lane; i < A; i += kWave) {
       const int r = i / W, c = i - (i / W) * W;
       const uint32_t code = cell_code(sR, sM, r, c, fc);
@@ -713,18 +721,45 @@ __device__ __forceinline__ void board_click(Pcg& rng, uint64_t& mine, uint64_t& 
   }
 }
 
+// Step outputs of one env in three store instructions, one per element width: lanes
+// 0..2 write the 4-byte fields (reward, step, last_new), lanes 0..1 the 1-byte fields
+// (done, outcome), lane 0 revealed_frac. Reported before the auto-reset (env.py:492-505).
+__device__ __forceinline__ void store_aux(const KParams& p, int64_t idx, int lane, double reward, bool done,
+                                          int32_t step_count, uint32_t newly, uint32_t total_rev, int outcome, int A) {
+  uint32_t* d4 = lane == 0 ? reinterpret_cast<uint32_t*>(p.reward)
+                           : (lane == 1 ? reinterpret_cast<uint32_t*>(p.step) : reinterpret_cast<uint32_t*>(p.last_new));
+  const uint32_t v4 = lane == 0 ? __float_as_uint((float)reward) : (lane == 1 ? (uint32_t)step_count : newly);
+  if (lane < 3 && d4) d4[idx] = v4;
+  uint8_t* d1 = lane == 0 ? p.done : reinterpret_cast<uint8_t*>(p.outcome);
+  const uint8_t v1 = lane == 0 ? (uint8_t)(done ? 1 : 0) : (uint8_t)(int8_t)outcome;
+  if (lane < 2 && d1) d1[idx] = v1;
+  if (lane == 0 && p.frac) p.frac[idx] = (double)total_rev / (double)(A > 1 ? A : 1);
+}
+
+// EnvMeta write-back in two 16-B stores: {st_hi, st_lo} and {has32, uinteger, step_count, flags}
+__device__ __forceinline__ void store_meta(EnvMeta* mp, const Pcg& rng, int32_t step_count, bool fc, int lane) {
+  if (lane == 0) {
+    *reinterpret_cast<ulonglong2*>(&mp->st_hi) = make_ulonglong2(rng.hi, rng.lo);
+    *reinterpret_cast<uint4*>(&mp->has32) =
+        make_uint4(rng.has32, rng.uinteger, (uint32_t)step_count, fc ? 1u : 0u);
+  }
+}
+
 // EPW boards per workgroup, one per wave, each with its own LDS slice: fewer,
 // larger workgroups halve the dispatch cost of a 4096-board launch, and no
 // wave ever waits on another (board code syncs with wave_sync only).
 template <int H_, int W_, int EPW>
-__global__ __launch_bounds__(64 * EPW, 8) void k_step(KParams p) {
+__global__ __launch_bounds__(64 * EPW) void k_step(KParams p) {
   __shared__ uint64_t sR_all[EPW][kWave];
   __shared__ uint64_t sM_all[EPW][kWave + 2];
   __shared__ uint32_t sTab_all[EPW][(H_ && W_) ? H_ * W_ : kMaxH * kMaxW];
   const int lane = lane_id();
   const int wv = (EPW == 1) ? 0 : (int)rfl(threadIdx.x >> 6);
-  const int64_t env = (int64_t)blockIdx.x * EPW + wv;
-  if (env >= p.n) return;
+  // A wave past the last env (tail of the last workgroup) loads env n-1 and leaves
+  // before any store: no early exit that would make every load wait for p.n.
+  const int64_t env_raw = (int64_t)blockIdx.x * EPW + wv;
+  const bool live = env_raw < p.n;
+  const int64_t env = live ? env_raw : p.n - 1;
   uint64_t* sR = sR_all[wv];
   uint64_t* sM = sM_all[wv];
   uint32_t* sTab = sTab_all[wv];
@@ -738,8 +773,20 @@ __global__ __launch_bounds__(64 * EPW, 8) void k_step(KParams p) {
   // issue every load up front
   uint64_t mine = load_row(mwords, g, lane);
   uint64_t rev = load_row(rwords, g, lane);
-  int64_t a = p.actions_i32 ? (int64_t)reinterpret_cast<const int32_t*>(p.actions)[env]
-                            : reinterpret_cast<const int64_t*>(p.actions)[env];
+  // jump-ahead entry k = lane+1 (2 KiB shared by every wave, L2-resident). Only a board
+  // whose next click is its first needs it, but every wave loads it here, right behind
+  // its rows: gating it on first_click_done would put a second dependent round trip on
+  // exactly the placement waves that end the launch. A placement consumes at most
+  // 2K-1 draws = K outputs, so only lanes < K need their entry.
+  uint64_t J[4] = {0ull, 0ull, 0ull, 0ull};
+  if (lane < p.K) {
+    const ulonglong2* e = reinterpret_cast<const ulonglong2*>(p.jump + 4 * lane);
+    const ulonglong2 a0 = e[0], a1 = e[1];
+    J[0] = a0.x;
+    J[1] = a0.y;
+    J[2] = a1.x;
+    J[3] = a1.y;
+  }
   Pcg rng;
   rng.hi = rfl64(mp->st_hi);
   rng.lo = rfl64(mp->st_lo);
@@ -749,24 +796,17 @@ __global__ __launch_bounds__(64 * EPW, 8) void k_step(KParams p) {
   rng.uinteger = rfl(mp->uinteger);
   int32_t step_count = (int32_t)rfl((uint32_t)mp->step_count);
   bool fc = (rfl(mp->flags) & 1u) != 0;
-  // jump-ahead entry k = lane+1 (2 KiB shared by every wave, L2-resident). Only
-  // a board whose next click is its first needs it, but it
-  // is loaded by every wave anyway, issued with the row loads: gating it on
-  // first_click_done would put a second dependent round trip on exactly the
-  // placement waves that end the launch
-  uint64_t J[4];
-  {
-    const ulonglong2* e = reinterpret_cast<const ulonglong2*>(p.jump + 4 * lane);
-    const ulonglong2 a0 = e[0], a1 = e[1];
-    J[0] = a0.x;
-    J[1] = a0.y;
-    J[2] = a1.x;
-    J[3] = a1.y;
-  }
+  // the action as two unconditional 4-B loads (int32: the element twice; int64: both
+  // halves): no branch, so they issue right behind the meta loads
+  const uint32_t* ap = reinterpret_cast<const uint32_t*>(p.actions);
+  const int64_t aw = p.actions_i32 ? env : 2 * env;
+  const uint32_t a_lo = ap[aw], a_hi = ap[p.actions_i32 ? aw : aw + 1];
+  int64_t a = p.actions_i32 ? (int64_t)(int32_t)a_lo : (int64_t)(((uint64_t)a_hi << 32) | a_lo);
   a = (int64_t)rfl64((uint64_t)a);
   int64_t cell64 = a % A;  // Python modulo (env.py:106)
   if (cell64 < 0) cell64 += A;
   const int cell = (int)cell64;
+  if (!live) return;
   STAMP(1);
 
   double reward = 0.0;
@@ -782,14 +822,7 @@ __global__ __launch_bounds__(64 * EPW, 8) void k_step(KParams p) {
   reward -= p.step_penalty;
   step_count += 1;
 
-  if (lane == 0) {  // aux is reported before the auto-reset (env.py:492-505)
-    if (p.reward) p.reward[env] = (float)reward;
-    if (p.done) p.done[env] = done ? 1 : 0;
-    if (p.step) p.step[env] = step_count;
-    if (p.last_new) p.last_new[env] = (int32_t)newly;
-    if (p.frac) p.frac[env] = (double)total_rev / (double)(A > 1 ? A : 1);
-    if (p.outcome) p.outcome[env] = (int8_t)outcome;
-  }
+  store_aux(p, env, lane, reward, done, step_count, newly, total_rev, outcome, A);
   if (done) {  // auto-reset (env.py:497-498 -> reset env.py:87-101); RNG continues
     mine = 0ull;
     rev = 0ull;
@@ -797,26 +830,19 @@ __global__ __launch_bounds__(64 * EPW, 8) void k_step(KParams p) {
     step_count = 0;
     mines_changed = true;
   }
-
-  // ---- persist state ----
-  if (lane == 0) {
-    mp->st_hi = rng.hi;
-    mp->st_lo = rng.lo;
-    mp->has32 = rng.has32;
-    mp->uinteger = rng.uinteger;
-    mp->step_count = step_count;
-    mp->flags = fc ? 1u : 0u;
-  }
-  if (mines_changed) store_rows(mwords, mine, sR, g, lane);
-  store_rows(rwords, rev, sR, g, lane);
   STAMP(4);
 
-  // ---- observation + action mask (env.py:172-196) ----
+  // ---- observation + action mask (env.py:172-196), issued before the state write-back:
+  // the obs stores are ~97 % of the bytes and the launch ends when they drain ----
   if (p.obs || p.mask) {
     stage_rows(sR, sM, rev, mine, g, lane);
     emit_obs(p.obs ? p.obs + env * 10 * A : nullptr, p.mask ? p.mask + env * A : nullptr, sR, sM,
-             fc, g, lane);
+             fc, g, lane, reinterpret_cast<uint8_t*>(sTab));
   }
+  // ---- persist state ----
+  store_meta(mp, rng, step_count, fc, lane);
+  if (mines_changed) store_rows(mwords, mine, sR, g, lane);
+  store_rows(rwords, rev, sR, g, lane);
   STAMP(5);
 }
 
@@ -1129,7 +1155,7 @@ __global__ __launch_bounds__(64) void k_late(KParams p, Pcg* lstate, LateCfg lc,
     if (p.obs || p.mask) {
       stage_rows(sR, sM, rev, mine, g, lane);
       emit_obs(p.obs ? p.obs + env * 10 * A : nullptr, p.mask ? p.mask + env * A : nullptr, sR, sM, fc, g,
-               lane);
+               lane, reinterpret_cast<uint8_t*>(sTab));
     }
     __syncthreads();
   }
@@ -1139,6 +1165,123 @@ __global__ __launch_bounds__(64) void k_late(KParams p, Pcg* lstate, LateCfg lc,
     lstate->has32 = L.has32;
     lstate->uinteger = L.uinteger;
   }
+}
+
+// ---------------------------------------------------------------------------
+// ms_run_tape: T consecutive (ms_tape_actions, ms_step) pairs in ONE launch.
+// A wave keeps its board in registers (rows in lanes, the PCG64 state in SGPRs)
+// for all T steps: per step it picks the tape action from the current board (the
+// rule of k_tape, evaluated wave-parallel: DPP sums, an exclusive scan and a
+// k-th-set-bit select), applies board_click, writes every output of the step,
+// auto-resets, and goes on. Meta and rows are read once and written once. With no
+// launch boundary between steps the waves drift apart, so one wave's obs stores
+// overlap another's flood fill. Bit-exact with the two-call sequence.
+// ---------------------------------------------------------------------------
+struct RunParams {
+  uint64_t t0;
+  int32_t T, mode, slots;
+  int64_t env_begin;
+  int64_t* actions;  // optional: the action of each step
+};
+
+template <int H_, int W_>
+__device__ __forceinline__ int tape_cell(uint64_t mine, uint64_t rev, const Geo<H_, W_>& g, int lane,
+                                         uint64_t gidx, uint64_t t, int mode) {
+  const uint64_t valid = ~rev & g.rowmask() & (lane < g.H ? ~0ull : 0ull);
+  const uint64_t x = splitmix64(0xC0FFEEull ^ (gidx << 32) ^ t);
+  uint64_t bits = valid;
+  uint32_t cnt = wave_sum((uint32_t)__popcll(valid));
+  uint64_t sel = x;
+  if (mode == MS_TAPE_SAFE_BIASED) {  // (uniform branch: mode is a kernel argument)
+    const uint64_t safe = valid & ~mine;
+    const uint32_t n_safe = wave_sum((uint32_t)__popcll(safe));
+    sel = x >> 16;
+    if ((x & 0xFFFFull) < 65208ull && n_safe > 0) {
+      bits = safe;
+      cnt = n_safe;
+    }
+  }
+  if (cnt == 0) return 0;
+  const uint32_t target = (uint32_t)(sel % (uint64_t)cnt);
+  const uint32_t pc = (uint32_t)__popcll(bits);
+  const uint32_t before = wave_excl_scan(pc);
+  const bool hit = target >= before && target < before + pc;
+  const uint64_t who = __ballot(hit);
+  const int src = __ffsll((unsigned long long)who) - 1;
+  const int col = (int)readlane32((uint32_t)(hit ? select_bit64(bits, target - before) : 0), src);
+  return src * g.W + col;
+}
+
+template <int H_, int W_, int EPW>
+__global__ __launch_bounds__(64 * EPW) void k_run(KParams p, RunParams r) {
+  __shared__ uint64_t sR_all[EPW][kWave];
+  __shared__ uint64_t sM_all[EPW][kWave + 2];
+  __shared__ uint32_t sTab_all[EPW][(H_ && W_) ? H_ * W_ : kMaxH * kMaxW];
+  const int lane = lane_id();
+  const int wv = (EPW == 1) ? 0 : (int)rfl(threadIdx.x >> 6);
+  const int64_t env = (int64_t)blockIdx.x * EPW + wv;
+  if (env >= p.n) return;
+  uint64_t* sR = sR_all[wv];
+  uint64_t* sM = sM_all[wv];
+  uint32_t* sTab = sTab_all[wv];
+  const Geo<H_, W_> g(p.H, p.W);
+  const int A = g.A(), NW = g.NW();
+  EnvMeta* mp = p.meta + env;
+  uint64_t* mwords = p.mine_words + env * NW;
+  uint64_t* rwords = p.rev_words + env * NW;
+  uint64_t mine = load_row(mwords, g, lane);
+  uint64_t rev = load_row(rwords, g, lane);
+  uint64_t J[4] = {0ull, 0ull, 0ull, 0ull};
+  if (lane < p.K) {
+    const ulonglong2* e = reinterpret_cast<const ulonglong2*>(p.jump + 4 * lane);
+    const ulonglong2 a0 = e[0], a1 = e[1];
+    J[0] = a0.x;
+    J[1] = a0.y;
+    J[2] = a1.x;
+    J[3] = a1.y;
+  }
+  Pcg rng;
+  rng.hi = rfl64(mp->st_hi);
+  rng.lo = rfl64(mp->st_lo);
+  rng.ihi = rfl64(mp->inc_hi);
+  rng.ilo = rfl64(mp->inc_lo);
+  rng.has32 = rfl(mp->has32);
+  rng.uinteger = rfl(mp->uinteger);
+  int32_t step_count = (int32_t)rfl((uint32_t)mp->step_count);
+  bool fc = (rfl(mp->flags) & 1u) != 0;
+  const uint64_t gidx = (uint64_t)(r.env_begin + env);
+  const int64_t n = p.n;
+  for (int t = 0; t < r.T; ++t) {
+    const int64_t slot = (r.slots ? (int64_t)t * n : 0) + env;
+    const int cell = tape_cell(mine, rev, g, lane, gidx, r.t0 + (uint64_t)t, r.mode);
+    double reward = 0.0;
+    bool done = false;
+    int outcome = MS_OUTCOME_NONE;
+    uint32_t newly = 0, total_rev = 0;
+    bool mines_changed = false;
+    board_click(rng, mine, rev, fc, cell, p, J, sTab, sR, g, lane, done, outcome, newly, total_rev, mines_changed);
+    if (outcome == MS_OUTCOME_LOSS) reward += p.loss_reward;
+    if (outcome == MS_OUTCOME_WIN) reward += p.win_reward;
+    reward -= p.step_penalty;
+    step_count += 1;
+    if (r.actions && lane == 0) r.actions[slot] = cell;
+    store_aux(p, slot, lane, reward, done, step_count, newly, total_rev, outcome, A);
+    if (done) {  // auto-reset; the RNG continues
+      mine = 0ull;
+      rev = 0ull;
+      fc = false;
+      step_count = 0;
+    }
+    if (p.obs || p.mask) {
+      stage_rows(sR, sM, rev, mine, g, lane);
+      emit_obs(p.obs ? p.obs + slot * 10 * A : nullptr, p.mask ? p.mask + slot * A : nullptr, sR, sM, fc, g, lane,
+               reinterpret_cast<uint8_t*>(sTab));
+    }
+    wave_sync();  // this step's LDS reads before the next step's placement / staging writes
+  }
+  store_meta(mp, rng, step_count, fc, lane);
+  store_rows(mwords, mine, sR, g, lane);
+  store_rows(rwords, rev, sR, g, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -1361,6 +1504,12 @@ void launch_step(const KParams& p, int epw, hipStream_t s) {
   } else {
     hipLaunchKernelGGL((k_step<H_, W_, 1>), dim3((unsigned)p.n), dim3(64), 0, s, p);
   }
+}
+
+template <int H_, int W_>
+void launch_run(const KParams& p, const RunParams& r, hipStream_t s) {
+  if (H_ && W_) hipLaunchKernelGGL((k_run<H_, W_, 4>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, p, r);
+  else hipLaunchKernelGGL((k_run<H_, W_, 1>), dim3((unsigned)p.n), dim3(64), 0, s, p, r);
 }
 
 template <int H_, int W_>
@@ -1608,6 +1757,42 @@ int ms_step(ms_handle* h, const int64_t* actions, float* obs, uint8_t* mask, flo
 int ms_step_i32(ms_handle* h, const int32_t* actions, float* obs, uint8_t* mask, float* reward, uint8_t* done,
                 int32_t* step, int32_t* last_new, double* revealed_frac, int8_t* outcome, void* stream) {
   return do_step(h, actions, 1, obs, mask, reward, done, step, last_new, revealed_frac, outcome, stream);
+}
+
+int ms_run_tape(ms_handle* h, uint64_t t0, int32_t T, int32_t mode, int32_t slots, int64_t* actions, float* obs,
+                uint8_t* mask, float* reward, uint8_t* done, int32_t* step, int32_t* last_new, double* revealed_frac,
+                int8_t* outcome, void* stream) {
+  if (!h) return fail(MS_EINVAL, "ms_run_tape: null handle");
+  if (T < 1) return fail(MS_EINVAL, "ms_run_tape: T must be >= 1");
+  if (mode != MS_TAPE_UNIFORM && mode != MS_TAPE_SAFE_BIASED) return fail(MS_EINVAL, "ms_run_tape: bad mode");
+  if (h->late_on) return fail(MS_EINVAL, "ms_run_tape: late-start resets are not supported");
+  KParams p = {};
+  fill_params(h, p);
+  p.actions = nullptr;
+  p.obs = obs;
+  p.mask = mask;
+  p.reward = reward;
+  p.done = done;
+  p.step = step;
+  p.last_new = last_new;
+  p.frac = revealed_frac;
+  p.outcome = outcome;
+  RunParams r;
+  r.t0 = t0;
+  r.T = T;
+  r.mode = mode;
+  r.slots = slots ? 1 : 0;
+  r.env_begin = h->env_begin;
+  r.actions = actions;
+  const hipStream_t s = (hipStream_t)stream;
+  if (h->H == 16 && h->W == 16) launch_run<16, 16>(p, r, s);
+  else if (h->H == 9 && h->W == 9) launch_run<9, 9>(p, r, s);
+  else if (h->H == 30 && h->W == 16) launch_run<30, 16>(p, r, s);
+  else if (h->H == 16 && h->W == 30) launch_run<16, 30>(p, r, s);
+  else if (h->H == 8 && h->W == 8) launch_run<8, 8>(p, r, s);
+  else launch_run<0, 0>(p, r, s);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? MS_OK : hip_fail(e, "ms_run_tape launch");
 }
 
 int ms_labels(ms_handle* h, float* mine_labels, uint8_t* mine_valid, void* stream) {

@@ -303,6 +303,27 @@ class VecMinesweeper:
             L.check(self._lib.ms_tape_actions(self._h, int(t), int(mode), L.ptr(out), self._stream()))
         return out
 
+    _RUN_KEYS = ("actions", "obs", "action_mask", "rewards", "dones", "step", "last_new_reveals",
+                 "revealed_frac", "outcome")
+
+    def run_tape(self, t0: int, T: int, mode: int = L.MS_TAPE_UNIFORM, slots: bool = True) -> Dict[str, torch.Tensor]:
+        """T synthetic-policy steps (tape_actions(t) then step, t = t0 .. t0+T-1) in ONE launch
+        (ms_run_tape: the boards stay in registers between steps). slots=True returns every
+        step's outputs stacked [T, N, ...]; slots=False only the last step's [N, ...].
+        Bit-exact with the loop; not available with late-start resets."""
+        n, A, dev = self.num_envs, self.H * self.W, self.device
+        lead = (int(T), n) if slots else (n,)
+        dt = {"actions": torch.int64, "obs": torch.float32, "action_mask": torch.bool, "rewards": torch.float32,
+              "dones": torch.bool, "step": torch.int32, "last_new_reveals": torch.int32,
+              "revealed_frac": torch.float64, "outcome": torch.int8}
+        tail = {"obs": (OBS_CHANNELS, self.H, self.W), "action_mask": (A,)}
+        out = {k: torch.empty(lead + tail.get(k, ()), dtype=dt[k], device=dev) for k in self._RUN_KEYS}
+        with torch.cuda.device(dev):
+            L.check(self._lib.ms_run_tape(self._h, int(t0), int(T), int(mode), 1 if slots else 0,
+                                          *(L.ptr(out[k]) for k in self._RUN_KEYS), self._stream()))
+        self._version += 1
+        return out
+
     def set_debug_flags(self, flags: int) -> None:
         """msenv_debug.h hooks (tests): e.g. L.MS_DBG_FORCE_SERIAL_PLACEMENT."""
         L.check(self._lib.ms_set_debug_flags(self._h, int(flags)))

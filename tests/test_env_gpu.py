@@ -243,3 +243,54 @@ def test_fixpoint_chain_and_serial_placement_agree(gpu, H, W, K):
         st = o.rng_state()
         for v in vs:
             assert np.array_equal(v.rng_state(), st), t
+
+
+_RUN_KEYS = ("actions", "obs", "action_mask", "rewards", "dones", "step", "last_new_reveals", "revealed_frac",
+             "outcome")
+
+
+@pytest.mark.parametrize("H,W,K", [(16, 16, 40), (9, 9, 10), (30, 16, 99), (16, 30, 99), (8, 8, 10), (5, 7, 8)])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_run_tape_equals_step_loop(gpu, H, W, K, mode):
+    """ms_run_tape (T tape steps in one launch, boards held in registers) is bit-exact with
+    T x (ms_tape_actions + ms_step); a second launch continues identically."""
+    N, T = 300, 40
+    a, b = _vec(H, W, K, N, seed=9), _vec(H, W, K, N, seed=9)
+    a.reset()
+    b.reset()
+    ref = {k: [] for k in _RUN_KEYS}
+    for t in range(2 * T):
+        act = a.tape_actions(7 + t, mode)
+        batch, r, d, info = a.step(act)
+        vals = dict(actions=act, obs=batch["obs"], action_mask=batch["action_mask"], rewards=r, dones=d,
+                    **{k: v for k, v in info.tensors.items() if k != "done"})
+        for k in _RUN_KEYS:
+            ref[k].append(vals[k].clone())
+    o1 = b.run_tape(7, T, mode, slots=True)
+    o2 = b.run_tape(7 + T, T, mode, slots=False)
+    for k in _RUN_KEYS:
+        assert torch.equal(torch.stack(ref[k][:T]), o1[k]), k
+        assert torch.equal(ref[k][-1], o2[k]), k
+    assert np.array_equal(a.rng_state(), b.rng_state())
+    sa, sb = a.snapshot_tensors(), b.snapshot_tensors()
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
+
+
+def test_run_tape_sharded_and_late_start(gpu):
+    from ms_amd import EnvConfig, VecMinesweeper
+    from ms_amd._lib import MsEnvError
+    cfg = EnvConfig(H=16, W=16, mine_count=40)
+    full = VecMinesweeper(512, cfg, seed=4)
+    parts = [VecMinesweeper(512, cfg, seed=4, shard=(r, 2)) for r in range(2)]
+    full.reset()
+    for p in parts:
+        p.reset()
+    of = full.run_tape(3, 25, 1, slots=False)
+    op = [p.run_tape(3, 25, 1, slots=False) for p in parts]
+    for k in _RUN_KEYS:
+        assert torch.equal(of[k], torch.cat([o[k] for o in op])), k
+    late = _vec(9, 9, 10, 8, late_start_cfg=dict(prob=0.5, min_hidden=3, max_hidden=20), late_start_seed=1)
+    late.reset()
+    with pytest.raises(MsEnvError):
+        late.run_tape(0, 4, 0)

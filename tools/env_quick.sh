@@ -11,3 +11,6 @@ for b in 9x9x10 30x16x99; do
   python -c "import json;d=json.load(open('gpurun_out/b_$b.json'));print('$b n 8192 value %.4g ms/step %.4f kern_ms %.4f frac %.3f'%(d['value'],d['ms_per_step'],d['roofline']['kernel_ms'],d['roofline']['frac']))"
 done
 timeout -k 10 200 python tools/diag_step.py --board 9x9x10 --envs 8192 > gpurun_out/diag9.txt 2>&1
+python -c "import json;d=json.load(open('gpurun_out/b_4096.json'))['multistep'];print('multistep 4096 value %.4g ms/step %.4f kern_ms %.4f frac %.3f'%(d['value'],d['ms_per_step'],d['roofline']['kernel_ms_per_step'],d['roofline']['frac']))"
+python -c "import json;d=json.load(open('gpurun_out/b_32768.json'))['multistep'];print('multistep 32768 value %.4g ms/step %.4f kern_ms %.4f frac %.3f'%(d['value'],d['ms_per_step'],d['roofline']['kernel_ms_per_step'],d['roofline']['frac']))"
+python -c "import json;d=json.load(open('gpurun_out/b_9x9x10.json'))['multistep'];print('multistep 9x9 value %.4g ms/step %.4f kern_ms %.4f frac %.3f'%(d['value'],d['ms_per_step'],d['roofline']['kernel_ms_per_step'],d['roofline']['frac']))"

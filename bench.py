@@ -35,17 +35,19 @@ def algo_bytes_per_env_step(H: int, W: int) -> int:
     return 40 * A + A + 8 + 4 + 1 + 12 + 2 * (2 * ((A + 7) // 8) + 32) + 16
 
 
-def pmc_traffic(H, W, K, n):
-    """HBM bytes per k_step launch from the committed rocprofv3 PMC passes
-    (FETCH_SIZE + WRITE_SIZE, separate passes; tools/profile_round.sh) of the
-    latest round under profiles/, for this exact board and env count."""
+def pmc_traffic(H, W, K, n, kernel="k_step"):
+    """HBM bytes per env step of all n envs (k_step: one launch; k_run: a launch / its
+    steps) from the committed rocprofv3 PMC passes (FETCH_SIZE + WRITE_SIZE, separate
+    passes; tools/profile_round.sh) of the latest round under profiles/, for this exact
+    board and env count."""
     import glob
-    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_k_step_{H}x{W}x{K}_{n}.json")))
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_{kernel}_{H}x{W}x{K}_{n}.json")))
     if not cands:
         return None, None
     with open(cands[-1]) as f:
         d = json.load(f)
-    return d["traffic_bytes_per_launch"], os.path.relpath(cands[-1], ROOT)
+    per_step = d.get("traffic_bytes_per_step", d["traffic_bytes_per_launch"])
+    return per_step, os.path.relpath(cands[-1], ROOT)
 
 
 def parse():
@@ -150,10 +152,12 @@ def multistep_bench(args, world, lib, h, L, n_local, n_total, H, W, bpe, dev):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, kern_ms = float(t[0]), float(t[1])
     achieved = bpe * n_local / (kern_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(H, W, args.board_k, n_local, "k_run")
     return {"metric": "env steps/sec, S synthetic-policy steps per launch (ms_run_tape)",
             "value": n_total * args.steps / el, "unit": "env_steps/s", "ms_per_step": el / args.steps * 1e3,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_run",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes per step",
+                         "traffic_source": traffic_src, "kernel": "k_run",
                          "kernel_ms_per_step": kern_ms, "steps_per_launch": S,
                          "kernel_ms_method": "HIP events around each S-step launch, summed / K"}}
 
@@ -210,6 +214,7 @@ def ppo_bench(args, world, rank, local_rank, dev):
 def main():
     args = parse()
     H, W, K = (int(x) for x in args.board.lower().split("x"))
+    args.board_k = K
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -37,6 +37,7 @@ ap.add_argument("--out", required=True)
 ap.add_argument("--config", default="16x16x40, 4096 envs, tape 0")
 ap.add_argument("--algo-bytes", type=int, default=4096 * 10729)
 ap.add_argument("--command", default="")
+ap.add_argument("--steps-per-launch", type=int, default=1, help="env steps one launch performs (k_run: S)")
 a = ap.parse_args()
 fe, wr = load(a.fetch, "FETCH_SIZE"), load(a.write, "WRITE_SIZE")
 allk = {}
@@ -49,7 +50,8 @@ fb = allk[name]["FETCH_SIZE_KB_mean"] * 1024
 wb = allk[name]["WRITE_SIZE_KB_mean"] * 1024
 out = {"command": a.command, "kernel": name, "config": a.config, "fetch_bytes_per_launch": fb,
        "write_bytes_per_launch": wb, "traffic_bytes_per_launch": fb + wb,
-       "algorithmic_bytes_per_launch": a.algo_bytes,
+       "algorithmic_bytes_per_launch": a.algo_bytes, "steps_per_launch": a.steps_per_launch,
+       "traffic_bytes_per_step": (fb + wb) / a.steps_per_launch,
        "note": "FETCH_SIZE taken as reported (small scattered state loads, not 16-B/lane streams); "
                "WRITE_SIZE exact for the dwordx4 obs stores",
        "all_kernels": allk}

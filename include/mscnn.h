@@ -25,14 +25,17 @@ extern "C" {
  *   out = relu(GN(y) * gamma + beta [+ res]) [* dmask[n][c]]
  * cin in {16, 96} (the stem's 10 input planes are zero-padded to 16).
  * res (bf16 [N][P][96]), dmask (f32 [N][96], 0 or 1/(1-p)), ysave and stats
- * (f32 [N][6][2] = mean, rstd per group) may be NULL. */
+ * (f32 [N][6][2] = mean, rstd per group) may be NULL. relu_mask (u8 [N][P][12],
+ * may be NULL) receives out > 0 as bits: bit j of byte (n, p, c8) is channel 8*c8 + j;
+ * the backward reads it instead of out (1/16 of the bytes). */
 int mc_conv_gn_fwd(const uint16_t* x, const uint16_t* w, const float* bias, const float* gamma,
                    const float* beta, const uint16_t* res, const float* dmask, uint16_t* out,
-                   uint16_t* ysave, float* stats, int32_t n, int32_t h, int32_t w_, int32_t cin,
-                   float eps, void* stream);
+                   uint16_t* ysave, float* stats, uint8_t* relu_mask, int32_t n, int32_t h, int32_t w_,
+                   int32_t cin, float eps, void* stream);
 
 /* Backward of one fused layer (the forward above with the same n, h, w, cin).
- * Inputs: dout = dL/d(out); out, ysave, stats from the forward; x = the forward's
+ * Inputs: dout = dL/d(out); out (or its relu_mask; the other may be NULL), ysave, stats
+ * from the forward; x = the forward's
  * input; wT = the conv weight re-laid out as bf16 [9][cin][96] (tap, ci, co), or
  * NULL when no input gradient is wanted (the stem: its input is the observation).
  * addend (bf16 [N][P][cin], may be NULL) is added to dx (the block input's skip
@@ -44,7 +47,8 @@ int mc_conv_gn_fwd(const uint16_t* x, const uint16_t* w, const float* bias, cons
  *   dgn    f32 [3][96]      d gamma, d beta, d bias.
  * work: f32 scratch of at least mc_conv_gn_bwd_workspace(...) floats.
  * Replaces autograd through cnn_residual.py:10-26, 50-54 (conv/GN/ReLU/Dropout2d). */
-int mc_conv_gn_bwd(const uint16_t* dout, const uint16_t* out, const uint16_t* ysave, const float* stats,
+int mc_conv_gn_bwd(const uint16_t* dout, const uint16_t* out, const uint8_t* relu_mask,
+                   const uint16_t* ysave, const float* stats,
                    const float* gamma, const float* dmask, const uint16_t* x, const uint16_t* wT,
                    const uint16_t* addend, uint16_t* dy, uint16_t* dz, uint16_t* dx, float* dw, float* dgn,
                    float* work, int64_t work_floats, int32_t n, int32_t h, int32_t w_, int32_t cin,

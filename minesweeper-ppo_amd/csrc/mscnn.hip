@@ -59,6 +59,7 @@ struct FwdParams {
   __bf16* out;
   __bf16* ysave;
   float* stats;
+  uint8_t* rmask;  // optional ReLU bitmask [N][P][12]: bit j of byte (px, c8) = out[px][8*c8 + j] > 0
   int N, H, W;
   float eps;
   int stagger;               // start delay of the upper half of the grid, 10-ns ticks (0 = none)
@@ -474,12 +475,15 @@ __global__ __launch_bounds__(256, PF ? 1 : (NPT <= 2 ? 2 : 1)) void k_conv_gn_fw
         if (PF) r8 = __builtin_bit_cast(bf16x8, rv[PF ? k : 0]);
         else if (p.res) r8 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(&p.res[o]));
         bf16x8 o8;
+        uint32_t mb = 0u;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float z = fmaxf((float)y8[j] * ca[k % 3][j] + cb[k % 3][j] + (float)r8[j], 0.f);
           o8[j] = (__bf16)(z * cd[k % 3][j]);
+          mb |= ((float)o8[j] > 0.f ? 1u : 0u) << j;
         }
         *reinterpret_cast<u32x4*>(&p.out[o]) = __builtin_bit_cast(u32x4, o8);
+        if (p.rmask) p.rmask[(size_t)n * P * (COUT / 8) + c] = (uint8_t)mb;
       }
     }
     FSTAMP(4);  // scale/shift + outputs issued
@@ -760,6 +764,7 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd_rw(FwdParams p) {
             rs = grstd[gg];
           }
         bf16x8 o8;
+        uint32_t mb = 0u;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int cl = ch * 8 + j;
@@ -768,8 +773,10 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd_rw(FwdParams p) {
           const float dm = sGB[2 * CH + cl];
           const float z = fmaxf((float)y8[j] * a + sh + (float)r8[j] * rsc, 0.f);
           o8[j] = (__bf16)(z * dm);
+          mb |= ((float)o8[j] > 0.f ? 1u : 0u) << j;
         }
         *reinterpret_cast<u32x4*>(&p.out[o]) = __builtin_bit_cast(u32x4, o8);
+        if (p.rmask) p.rmask[((size_t)n * P + px) * (COUT / 8) + co0 / 8 + ch] = (uint8_t)mb;
       }
     }
     FSTAMP(4);
@@ -847,8 +854,8 @@ void mc_set_fwd_diag(unsigned long long* d) { g_fwd_diag = d; }
 #endif
 
 int mc_conv_gn_fwd(const uint16_t* x, const uint16_t* w, const float* bias, const float* gamma, const float* beta,
-                   const uint16_t* res, const float* dmask, uint16_t* out, uint16_t* ysave, float* stats, int32_t n,
-                   int32_t h, int32_t w_, int32_t cin, float eps, void* stream) {
+                   const uint16_t* res, const float* dmask, uint16_t* out, uint16_t* ysave, float* stats,
+                   uint8_t* relu_mask, int32_t n, int32_t h, int32_t w_, int32_t cin, float eps, void* stream) {
   if (!x || !w || !bias || !gamma || !beta || !out || n <= 0 || h <= 0 || w_ <= 0) {
     snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd: bad argument");
     return MS_EINVAL;
@@ -864,6 +871,7 @@ int mc_conv_gn_fwd(const uint16_t* x, const uint16_t* w, const float* bias, cons
   p.out = reinterpret_cast<__bf16*>(out);
   p.ysave = reinterpret_cast<__bf16*>(ysave);
   p.stats = stats;
+  p.rmask = relu_mask;
   p.N = n;
   p.H = h;
   p.W = w_;

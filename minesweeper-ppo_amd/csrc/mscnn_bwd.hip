@@ -4,7 +4,8 @@
 //   y = conv3x3(x, w) + bias;  z = GN(y) * gamma + beta [+ res];  out = relu(z) [* dmask]
 // Backward, per layer, in two persistent kernels:
 //   k_bwd_data  (one workgroup per sample at a time, 2 workgroups per CU)
-//     pass 1: dz = (out > 0) * dout * dmask  and the per-channel sums
+//     pass 1: dz = (out > 0) * dout * dmask  and the per-channel sums (out > 0 read
+//             as the forward's ReLU bitmask, 1/16 of out's bytes, when one is given)
 //             S1 = sum dz, S2 = sum dz*yhat, S3 = sum yhat (yhat = (y - mean) * rstd);
 //     pass 2: dy = rstd*gamma*dz - rstd*mean_g(gamma*dz) - rstd*yhat*mean_g(gamma*dz*yhat)
 //             (GroupNorm backward), kept in an LDS tile and stored for k_wgrad;
@@ -40,6 +41,7 @@ constexpr int NC8 = COUT / 8;  // 16-byte chunks per 96-channel pixel row
 struct BwdDataParams {
   const __bf16* dout;
   const __bf16* out;
+  const uint8_t* rmask;  // ReLU bitmask of the forward (replaces the sign test on out), or NULL
   const __bf16* y;
   const float* stats;
   const float* gamma;
@@ -125,15 +127,18 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
 #pragma unroll
     for (int i0 = 0; i0 < NCH; i0 += LB) {
       u32x4 dv[LB], ov[LB];
+      uint32_t mv[LB];
 #pragma unroll
       for (int u = 0; u < LB; ++u) {
         const int i = i0 + u, px = pg + PG * i;
         if (i < NCH) yr[i] = u32x4{0u, 0u, 0u, 0u};
+        mv[u] = 0u;
         if (i < NCH && gact && px < P) {
           const size_t o = ((size_t)n * P + px) * COUT + c8 * 8;
 #ifndef MC_EXP_B_NO_P1LOAD
           dv[u] = *reinterpret_cast<const u32x4*>(&p.dout[o]);
-          ov[u] = *reinterpret_cast<const u32x4*>(&p.out[o]);
+          if (p.rmask) mv[u] = p.rmask[((size_t)n * P + px) * NC8 + c8];
+          else ov[u] = *reinterpret_cast<const u32x4*>(&p.out[o]);
           yr[i] = *reinterpret_cast<const u32x4*>(&p.y[o]);
 #else
           dv[u] = u32x4{(unsigned)o, 1u, 2u, 3u};
@@ -146,13 +151,19 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
       for (int u = 0; u < LB; ++u) {
         const int i = i0 + u, px = pg + PG * i;
         if (i < NCH && gact && px < P) {
-          const bf16x8 d8 = __builtin_bit_cast(bf16x8, dv[u]), o8 = __builtin_bit_cast(bf16x8, ov[u]);
+          const bf16x8 d8 = __builtin_bit_cast(bf16x8, dv[u]);
           const bf16x8 y8 = __builtin_bit_cast(bf16x8, yr[i]);
+          uint32_t pos = mv[u];
+          if (!p.rmask) {  // (uniform)
+            const bf16x8 o8 = __builtin_bit_cast(bf16x8, ov[u]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) pos |= ((float)o8[j] > 0.f ? 1u : 0u) << j;
+          }
           bf16x8 z8;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const float d = (float)d8[j] * dm[j];
-            z8[j] = (__bf16)((float)o8[j] > 0.f ? d : 0.f);
+            z8[j] = (__bf16)(((pos >> j) & 1u) ? d : 0.f);
             const float zf = (float)z8[j];
             const float yh = ((float)y8[j] - mean) * rstd;
             s1[j] += zf;
@@ -584,12 +595,13 @@ int64_t mc_conv_gn_bwd_workspace(int32_t n, int32_t h, int32_t w_, int32_t cin) 
   return pl.gn_part + pl.w_part;
 }
 
-int mc_conv_gn_bwd(const uint16_t* dout, const uint16_t* out, const uint16_t* ysave, const float* stats,
+int mc_conv_gn_bwd(const uint16_t* dout, const uint16_t* out, const uint8_t* relu_mask, const uint16_t* ysave,
+                   const float* stats,
                    const float* gamma, const float* dmask, const uint16_t* x, const uint16_t* wT,
                    const uint16_t* addend, uint16_t* dy, uint16_t* dz, uint16_t* dx, float* dw, float* dgn,
                    float* work, int64_t work_floats, int32_t n, int32_t h, int32_t w_, int32_t cin,
                    void* stream) {
-  if (!dout || !out || !ysave || !stats || !gamma || !x || !dy || !dw || !dgn || !work || n <= 0 || h <= 0 ||
+  if (!dout || (!out && !relu_mask) || !ysave || !stats || !gamma || !x || !dy || !dw || !dgn || !work || n <= 0 || h <= 0 ||
       w_ <= 0) {
     snprintf(g_err, sizeof g_err, "mc_conv_gn_bwd: bad argument");
     return MS_EINVAL;
@@ -616,6 +628,7 @@ int mc_conv_gn_bwd(const uint16_t* dout, const uint16_t* out, const uint16_t* ys
   BwdDataParams bp;
   bp.dout = reinterpret_cast<const __bf16*>(dout);
   bp.out = reinterpret_cast<const __bf16*>(out);
+  bp.rmask = relu_mask;
   bp.y = reinterpret_cast<const __bf16*>(ysave);
   bp.stats = stats;
   bp.gamma = gamma;

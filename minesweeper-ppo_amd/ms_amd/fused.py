@@ -57,12 +57,12 @@ def obs_to_nhwc(obs: torch.Tensor, cin_pad: int = 16) -> torch.Tensor:
 
 def conv_gn_fwd(x: torch.Tensor, wt: torch.Tensor, bias: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor,
                 H: int, W: int, res: Optional[torch.Tensor] = None, dmask: Optional[torch.Tensor] = None,
-                save: bool = True, eps: float = 1e-5
-                ) -> Tuple[torch.Tensor, Optional[torch.Tensor], Optional[torch.Tensor]]:
-    """out = relu(GN(conv3x3(x) + bias) * gamma + beta [+ res]) [* dmask]; returns (out, y, stats)."""
+                save: bool = True, eps: float = 1e-5, want_mask: bool = False):
+    """out = relu(GN(conv3x3(x) + bias) * gamma + beta [+ res]) [* dmask]; returns (out, y, stats),
+    plus the ReLU bitmask (u8 [N, P, 12], bit j of byte c8 = out[..., 8*c8 + j] > 0) with want_mask."""
     global _fwd
     if _fwd is None:
-        _fwd = _fn("mc_conv_gn_fwd", [_vp] * 10 + [_i32] * 4 + [_f32, _vp])
+        _fwd = _fn("mc_conv_gn_fwd", [_vp] * 11 + [_i32] * 4 + [_f32, _vp])
     n, p, cin = x.shape
     assert p == H * W and x.dtype == torch.bfloat16 and x.is_contiguous()
     assert wt.shape == (9, COUT, cin) and wt.dtype == torch.bfloat16 and wt.is_contiguous()
@@ -70,6 +70,7 @@ def conv_gn_fwd(x: torch.Tensor, wt: torch.Tensor, bias: torch.Tensor, gamma: to
     out = torch.empty((n, p, COUT), dtype=torch.bfloat16, device=dev)
     y = torch.empty_like(out) if save else None
     stats = torch.empty((n, NGROUPS, 2), dtype=torch.float32, device=dev) if save else None
+    rmask = torch.empty((n, p, COUT // 8), dtype=torch.uint8, device=dev) if want_mask else None
     if res is not None:
         assert res.shape == out.shape and res.dtype == torch.bfloat16 and res.is_contiguous()
     if dmask is not None:
@@ -78,8 +79,8 @@ def conv_gn_fwd(x: torch.Tensor, wt: torch.Tensor, bias: torch.Tensor, gamma: to
     f32c = lambda t: t.detach().to(torch.float32).contiguous()  # noqa: E731
     b, g, be = f32c(bias), f32c(gamma), f32c(beta)
     _check(_fwd(L.ptr(x), L.ptr(wt), L.ptr(b), L.ptr(g), L.ptr(be), L.ptr(res), L.ptr(dmask), L.ptr(out),
-                L.ptr(y), L.ptr(stats), n, H, W, cin, eps, L.stream_ptr(dev)))
-    return out, y, stats
+                L.ptr(y), L.ptr(stats), L.ptr(rmask), n, H, W, cin, eps, L.stream_ptr(dev)))
+    return (out, y, stats, rmask) if want_mask else (out, y, stats)
 
 
 _bwd = None
@@ -97,20 +98,25 @@ def dw_to_conv(dw: torch.Tensor, cin_real: int) -> torch.Tensor:
     return dw.view(3, 3, COUT, dw.shape[-1]).permute(2, 3, 0, 1)[:, :cin_real].contiguous()
 
 
-def conv_gn_bwd(dout: torch.Tensor, out: torch.Tensor, y: torch.Tensor, stats: torch.Tensor, gamma: torch.Tensor,
-                x: torch.Tensor, H: int, W: int, wT: Optional[torch.Tensor] = None,
-                dmask: Optional[torch.Tensor] = None, addend: Optional[torch.Tensor] = None, want_dz: bool = False):
+def conv_gn_bwd(dout: torch.Tensor, out: Optional[torch.Tensor], y: torch.Tensor, stats: torch.Tensor,
+                gamma: torch.Tensor, x: torch.Tensor, H: int, W: int, wT: Optional[torch.Tensor] = None,
+                dmask: Optional[torch.Tensor] = None, addend: Optional[torch.Tensor] = None, want_dz: bool = False,
+                rmask: Optional[torch.Tensor] = None):
     """Backward of conv_gn_fwd. Returns (dx | None, dz | None, dw f32 [9,96,cin], dgn f32 [3,96] =
-    d gamma, d beta, d bias). dx (bf16, NHWC) is produced iff the dgrad weights ``wT`` are given."""
+    d gamma, d beta, d bias). dx (bf16, NHWC) is produced iff the dgrad weights ``wT`` are given.
+    ``rmask`` (the forward's ReLU bitmask) replaces the sign test on ``out``; one of them is needed."""
     global _bwd, _bwd_ws
     if _bwd is None:
-        _bwd = _fn("mc_conv_gn_bwd", [_vp] * 15 + [ctypes.c_int64] + [_i32] * 4 + [_vp])
+        _bwd = _fn("mc_conv_gn_bwd", [_vp] * 16 + [ctypes.c_int64] + [_i32] * 4 + [_vp])
         _bwd_ws = _fn("mc_conv_gn_bwd_workspace", [_i32] * 4)
         _bwd_ws.restype = ctypes.c_int64
     n, p, cin = x.shape
     dev = x.device
+    assert out is not None or rmask is not None
     for t in (dout, out, y):
-        assert t.shape == (n, p, COUT) and t.dtype == torch.bfloat16 and t.is_contiguous()
+        assert t is None or (t.shape == (n, p, COUT) and t.dtype == torch.bfloat16 and t.is_contiguous())
+    if rmask is not None:
+        assert rmask.shape == (n, p, COUT // 8) and rmask.dtype == torch.uint8 and rmask.is_contiguous()
     assert x.dtype == torch.bfloat16 and x.is_contiguous() and p == H * W
     assert stats.shape == (n, NGROUPS, 2) and stats.dtype == torch.float32
     if wT is not None:
@@ -129,7 +135,7 @@ def conv_gn_bwd(dout: torch.Tensor, out: torch.Tensor, y: torch.Tensor, stats: t
     if nws < 0:
         raise L.MsEnvError("mc_conv_gn_bwd_workspace: bad sizes")
     work = torch.empty(nws, dtype=torch.float32, device=dev)
-    _check(_bwd(L.ptr(dout), L.ptr(out), L.ptr(y), L.ptr(stats), L.ptr(g), L.ptr(dmask), L.ptr(x), L.ptr(wT),
+    _check(_bwd(L.ptr(dout), L.ptr(out), L.ptr(rmask), L.ptr(y), L.ptr(stats), L.ptr(g), L.ptr(dmask), L.ptr(x), L.ptr(wT),
                 L.ptr(addend), L.ptr(dy), L.ptr(dz), L.ptr(dx), L.ptr(dw), L.ptr(dgn), L.ptr(work), nws,
                 n, H, W, cin, L.stream_ptr(dev)))
     return dx, dz, dw, dgn
@@ -163,8 +169,8 @@ def trunk_layers(model) -> list:
 
 def _trunk_forward(x0, layers, H, W, dmasks, save):
     """Runs every layer; with ``save`` returns the tensors the backward needs:
-    acts[l] = input of layer l (acts[l + 1] = its output), ys[l], sts[l]."""
-    acts, ys, sts = [x0], [], []
+    acts[l] = input of layer l (acts[l + 1] = its output), ys[l], sts[l], and the ReLU bitmasks."""
+    acts, ys, sts, rms = [x0], [], [], []
     x, blk_in = x0, None
     for li, (conv, norm) in enumerate(layers):
         wt = _packed(conv.weight, "f", x.shape[-1])
@@ -174,27 +180,31 @@ def _trunk_forward(x0, layers, H, W, dmasks, save):
             dm = dmasks[(li - 1) // 2] if dmasks is not None else None
         elif li > 0:  # second half: + the block input, then ReLU
             res = blk_in
-        x, y, st = conv_gn_fwd(x, wt, conv.bias, norm.weight, norm.bias, H, W, res=res, dmask=dm, save=save,
-                               eps=norm.eps)
         if save:
+            x, y, st, rm = conv_gn_fwd(x, wt, conv.bias, norm.weight, norm.bias, H, W, res=res, dmask=dm,
+                                       save=True, eps=norm.eps, want_mask=True)
             acts.append(x)
             ys.append(y)
             sts.append(st)
-    return x, acts, ys, sts
+            rms.append(rm)
+        else:
+            x, _, _ = conv_gn_fwd(x, wt, conv.bias, norm.weight, norm.bias, H, W, res=res, dmask=dm,
+                                  save=False, eps=norm.eps)
+    return x, acts, ys, sts, rms
 
 
 class _TrunkFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x0, H, W, dmasks, layers, *params):
-        out, acts, ys, sts = _trunk_forward(x0, layers, H, W, dmasks, save=True)
+        out, acts, ys, sts, rms = _trunk_forward(x0, layers, H, W, dmasks, save=True)
         ctx.H, ctx.W, ctx.layers, ctx.dmasks = H, W, layers, dmasks
-        ctx.saved = (acts, ys, sts)
+        ctx.saved = (acts, ys, sts, rms)
         ctx.nparams = len(params)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        acts, ys, sts = ctx.saved
+        acts, ys, sts, rms = ctx.saved
         layers, H, W, dmasks = ctx.layers, ctx.H, ctx.W, ctx.dmasks
         grads = {}
         d = dout.to(torch.bfloat16).contiguous()
@@ -207,9 +217,9 @@ class _TrunkFn(torch.autograd.Function):
             want_dx = li > 0
             dm = dmasks[(li - 1) // 2] if (dmasks is not None and li % 2 == 1) else None
             addend = skip if li % 2 == 1 else None
-            dx, dz, dw, dgn = conv_gn_bwd(d, acts[li + 1], ys[li], sts[li], norm.weight, x, H, W,
+            dx, dz, dw, dgn = conv_gn_bwd(d, None, ys[li], sts[li], norm.weight, x, H, W,
                                           wT=_packed(conv.weight, "t") if want_dx else None, dmask=dm,
-                                          addend=addend, want_dz=(li % 2 == 0 and li > 0))
+                                          addend=addend, want_dz=(li % 2 == 0 and li > 0), rmask=rms[li])
             skip = dz
             grads[id(conv.weight)] = dw_to_conv(dw, cin_real)
             grads[id(conv.bias)] = dgn[2]
@@ -244,7 +254,7 @@ def fused_features(model, obs: torch.Tensor) -> torch.Tensor:
     params = trunk_params(layers)
     if torch.is_grad_enabled() and any(q.requires_grad for q in params):
         return _TrunkFn.apply(x0, H, W, dmasks, layers, *params)
-    out, _, _, _ = _trunk_forward(x0, layers, H, W, dmasks, save=False)
+    out, _, _, _, _ = _trunk_forward(x0, layers, H, W, dmasks, save=False)
     return out
 
 

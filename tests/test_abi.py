@@ -54,8 +54,8 @@ def test_cnn_entry_points_validate_arguments():
     assert lib.mc_conv_gn_bwd_workspace(0, 16, 16, 96) == -1
     assert lib.mc_conv_gn_bwd_workspace(4, 16, 16, 32) == -1  # cin 16 or 96 only
     vp = ctypes.c_void_p
-    lib.mc_conv_gn_fwd.argtypes = [vp] * 10 + [ctypes.c_int32] * 4 + [ctypes.c_float, vp]
-    assert lib.mc_conv_gn_fwd(*([None] * 10), 4, 16, 16, 96, 1e-5, None) == 1
+    lib.mc_conv_gn_fwd.argtypes = [vp] * 11 + [ctypes.c_int32] * 4 + [ctypes.c_float, vp]
+    assert lib.mc_conv_gn_fwd(*([None] * 11), 4, 16, 16, 96, 1e-5, None) == 1
     assert b"bad argument" in lib.mc_last_error()
 
 

@@ -46,11 +46,14 @@ def test_conv_gn_fwd_matches_torch(gpu, H, W, cin, n, with_res, rw, monkeypatch)
     b, g, be = torch.randn(96, device=gpu) * 0.1, 1 + 0.1 * torch.randn(96, device=gpu), 0.1 * torch.randn(96, device=gpu)
     res = torch.randn(n, P, 96, device=gpu).to(torch.bfloat16) if with_res else None
     dmask = ((torch.rand(n, 96, device=gpu) > 0.05).float() / 0.95) if not with_res else None
-    out, y, st = conv_gn_fwd(x, prep_weight(w, cin), b, g, be, H, W, res=res, dmask=dmask)
+    out, y, st, rm = conv_gn_fwd(x, prep_weight(w, cin), b, g, be, H, W, res=res, dmask=dmask, want_mask=True)
     ro, ry, rst = _ref(x, w, b, g, be, H, W, res, dmask)
     torch.testing.assert_close(y.float(), ry, atol=2e-2, rtol=2e-2)
     torch.testing.assert_close(st, rst, atol=1e-3, rtol=1e-3)
     torch.testing.assert_close(out.float(), ro, atol=3e-2, rtol=2e-2)
+    # the ReLU bitmask is exactly out > 0 (bit j of byte c8 = channel 8*c8 + j)
+    bits = (rm.to(torch.int32)[..., None] >> torch.arange(8, device=gpu, dtype=torch.int32)) & 1
+    assert torch.equal(bits.reshape(n, P, 96).bool(), out.float() > 0)
 
 
 def _rel(a, b):
@@ -91,6 +94,12 @@ def test_conv_gn_bwd_matches_torch(gpu, H, W, cin, n, with_res):
     add = torch.randn(n, P, cin, device=gpu).to(torch.bfloat16) if (with_res and want_dx) else None
     dx, dz, dw, dgn = conv_gn_bwd(dout, out, y, st, g, x, H, W, wT=prep_weight_t(w) if want_dx else None,
                                   dmask=dmask, addend=add, want_dz=with_res)
+    # the bitmask path (what the trunk uses) gives bit-identical gradients
+    rm = conv_gn_fwd(x, prep_weight(w, cin), b, g, be, H, W, res=res, dmask=dmask, want_mask=True)[3]
+    got = conv_gn_bwd(dout, None, y, st, g, x, H, W, wT=prep_weight_t(w) if want_dx else None,
+                      dmask=dmask, addend=add, want_dz=with_res, rmask=rm)
+    for a_, b_ in zip((dx, dz, dw, dgn), got):
+        assert (a_ is None and b_ is None) or torch.equal(a_, b_)
     nchw = lambda t, c: t.float().view(n, H, W, c).permute(0, 3, 1, 2).contiguous()  # noqa: E731
     nhwc = lambda t: t.permute(0, 2, 3, 1).reshape(n, P, -1)  # noqa: E731
     xr = nchw(x, cin)

@@ -375,7 +375,10 @@ __host__ __device__ inline int wgrad_lds(int H, int W) {
 
 // One wave's share of the 27 (tap, co-tile) 32x32 tiles of a 32-wide ci slice: tiles
 // [T0, T0+NT) in tap-major order, so a wave touches at most 3 taps.
-template <int CIN, int T0, int NT>
+// PF (16x16 boards, 96 channels): the next sample's dy and x slice are loaded into
+// registers (12 + 4 16-B chunks per thread) while this sample's MFMAs run, and written
+// to LDS after the trailing barrier, so the load round trip leaves the critical path.
+template <int CIN, int T0, int NT, bool PF>
 __device__ __forceinline__ void wgrad_body(const WgradParams& p, __bf16* sDY, __bf16* sX, int gid, int ci0) {
   constexpr int TAP0 = T0 / 3, TAP1 = (T0 + NT - 1) / 3, NTAP = TAP1 - TAP0 + 1;
   constexpr int XC = CIN < 32 ? CIN : 32;  // real channels of the slice (the stem's 16 + 16 zero)
@@ -398,18 +401,47 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, __bf16* sDY, __
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
 
-  for (int n = gid; n < p.N; n += p.G) {
-    const u32x4* dys = reinterpret_cast<const u32x4*>(p.dy + (size_t)n * P * COUT);
-#pragma unroll 4
-    for (int c = tid; c < P * NC8; c += 256) *reinterpret_cast<u32x4*>(&sDY[c * 8]) = dys[c];
-#pragma unroll 2
-    for (int c = tid; c < P * XCH; c += 256) {
-      const int px = c / XCH, k = c - px * XCH;
-      const int r = px / W, cc = px - r * W;
-      *reinterpret_cast<u32x4*>(&sX[((r + 1) * WP + cc + 1) * 32 + k * 8]) =
-          *reinterpret_cast<const u32x4*>(&p.x[((size_t)n * P + px) * CIN + ci0 + k * 8]);
+  constexpr int NDY = PF ? 256 * NC8 / 256 : 1, NXS = PF ? 256 * XCH / 256 : 1;
+  u32x4 rdy[NDY], rx[NXS];
+  auto prefetch = [&](int n) {  // PF: P == 256, W == 16
+    if (n < p.N) {
+      const u32x4* dys = reinterpret_cast<const u32x4*>(p.dy + (size_t)n * 256 * COUT);
+#pragma unroll
+      for (int k = 0; k < NDY; ++k) rdy[k] = dys[tid + 256 * k];
+#pragma unroll
+      for (int k = 0; k < NXS; ++k) {
+        const int c = tid + 256 * k, px = c / XCH, kk = c - px * XCH;
+        rx[k] = *reinterpret_cast<const u32x4*>(&p.x[((size_t)n * 256 + px) * CIN + ci0 + kk * 8]);
+      }
     }
-    __syncthreads();
+  };
+  if (PF) prefetch(gid);
+  for (int n = gid; n < p.N; n += p.G) {
+    if (PF) {
+#pragma unroll
+      for (int k = 0; k < NDY; ++k) *reinterpret_cast<u32x4*>(&sDY[(tid + 256 * k) * 8]) = rdy[k];
+#pragma unroll
+      for (int k = 0; k < NXS; ++k) {
+        const int c = tid + 256 * k, px = c / XCH, kk = c - px * XCH;
+        const int r = px >> 4, cc = px & 15;
+        *reinterpret_cast<u32x4*>(&sX[((r + 1) * 18 + cc + 1) * 32 + kk * 8]) = rx[k];
+      }
+      __syncthreads();
+      prefetch(n + p.G);
+      asm volatile("" ::: "memory");  // the prefetch is issued before the MFMA loop
+    } else {
+      const u32x4* dys = reinterpret_cast<const u32x4*>(p.dy + (size_t)n * P * COUT);
+#pragma unroll 4
+      for (int c = tid; c < P * NC8; c += 256) *reinterpret_cast<u32x4*>(&sDY[c * 8]) = dys[c];
+#pragma unroll 2
+      for (int c = tid; c < P * XCH; c += 256) {
+        const int px = c / XCH, k = c - px * XCH;
+        const int r = px / W, cc = px - r * W;
+        *reinterpret_cast<u32x4*>(&sX[((r + 1) * WP + cc + 1) * 32 + k * 8]) =
+            *reinterpret_cast<const u32x4*>(&p.x[((size_t)n * P + px) * CIN + ci0 + k * 8]);
+      }
+      __syncthreads();
+    }
     for (int k0 = 0; k0 < Ppad; k0 += 16) {
       bf16x8 a[3];
 #pragma unroll
@@ -450,7 +482,7 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, __bf16* sDY, __
   }
 }
 
-template <int CIN>
+template <int CIN, bool PF>
 __global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NCI = CIN / 32 > 0 ? CIN / 32 : 1;
@@ -467,10 +499,10 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   stagger_start(p.stagger);
   switch (wave) {
-    case 0: wgrad_body<CIN, 0, 7>(p, sDY, sX, gid, cig * 32); break;
-    case 1: wgrad_body<CIN, 7, 7>(p, sDY, sX, gid, cig * 32); break;
-    case 2: wgrad_body<CIN, 14, 7>(p, sDY, sX, gid, cig * 32); break;
-    default: wgrad_body<CIN, 21, 6>(p, sDY, sX, gid, cig * 32); break;
+    case 0: wgrad_body<CIN, 0, 7, PF>(p, sDY, sX, gid, cig * 32); break;
+    case 1: wgrad_body<CIN, 7, 7, PF>(p, sDY, sX, gid, cig * 32); break;
+    case 2: wgrad_body<CIN, 14, 7, PF>(p, sDY, sX, gid, cig * 32); break;
+    default: wgrad_body<CIN, 21, 6, PF>(p, sDY, sX, gid, cig * 32); break;
   }
 }
 
@@ -566,14 +598,24 @@ int dispatch_bwd_data(const BwdDataParams& p, int grid, hipStream_t s) {
   return MS_OK;
 }
 
-template <int CIN>
-void launch_wgrad(const WgradParams& p, int grid, size_t lds, hipStream_t s) {
+template <int CIN, bool PF>
+void launch_wgrad_t(const WgradParams& p, int grid, size_t lds, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    set_lds_attr(k_wgrad<CIN>);
+    set_lds_attr(k_wgrad<CIN, PF>);
     attr = true;
   }
-  hipLaunchKernelGGL((k_wgrad<CIN>), dim3(grid), dim3(256), lds, s, p);
+  hipLaunchKernelGGL((k_wgrad<CIN, PF>), dim3(grid), dim3(256), lds, s, p);
+}
+
+template <int CIN>
+void launch_wgrad(const WgradParams& p, int grid, size_t lds, hipStream_t s) {
+  // MC_WG_PF=0 turns the register prefetch of the 16x16 96-channel case off (A/B)
+  static const bool pf = getenv("MC_WG_PF") ? atoi(getenv("MC_WG_PF")) != 0 : true;
+  if constexpr (CIN == 96) {
+    if (pf && p.H == 16 && p.W == 16) return launch_wgrad_t<CIN, true>(p, grid, lds, s);
+  }
+  launch_wgrad_t<CIN, false>(p, grid, lds, s);
 }
 
 int check_launch(const char* what) {

@@ -442,6 +442,38 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, __bf16* sDY, __
       }
       __syncthreads();
     }
+    if (PF) {
+      // 16 pixel steps, operands double-buffered: step k+1's LDS reads are issued
+      // before step k's MFMAs
+      auto ld = [&](int k0, bf16x8 (&a)[3], bf16x8 (&b)[NTAP]) {
+#pragma unroll
+        for (int cot = 0; cot < 3; ++cot) {
+          const __bf16* base = sDY + (k0 + rowoff) * COUT + cot * 32 + col;
+          a[cot] = cat8(lds_tr4(base), lds_tr4(base + 4 * COUT));
+        }
+        const int px0 = k0 + rowoff, px1 = px0 + 4;
+        const int h0 = ((px0 >> 4) + 1) * 18 + (px0 & 15) + 1, h1 = ((px1 >> 4) + 1) * 18 + (px1 & 15) + 1;
+#pragma unroll
+        for (int j = 0; j < NTAP; ++j)
+          b[j] = cat8(lds_tr4(sX + h0 * 32 + tapoff[j] + col), lds_tr4(sX + h1 * 32 + tapoff[j] + col));
+      };
+      auto mm = [&](const bf16x8 (&a)[3], const bf16x8 (&b)[NTAP]) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const int tt = T0 + t;
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[tt % 3], b[tt / 3 - TAP0], acc[t], 0, 0, 0);
+        }
+      };
+      bf16x8 a0[3], b0[NTAP], a1[3], b1[NTAP];
+      ld(0, a0, b0);
+#pragma unroll
+      for (int k0 = 0; k0 < 256; k0 += 32) {
+        ld(k0 + 16, a1, b1);
+        mm(a0, b0);
+        if (k0 + 32 < 256) ld(k0 + 32, a0, b0);
+        mm(a1, b1);
+      }
+    } else
     for (int k0 = 0; k0 < Ppad; k0 += 16) {
       bf16x8 a[3];
 #pragma unroll

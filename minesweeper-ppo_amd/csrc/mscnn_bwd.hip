@@ -290,18 +290,36 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
         const bool v = (unsigned)sr < (unsigned)H && (unsigned)sc < (unsigned)W;
         aoff[t] = (v ? sr * W + sc : P) * DCP + 8 * hh;
       }
-#pragma unroll
-      for (int k0 = 0; k0 < COUT; k0 += 16) {
-        bf16x8 b[3];
+      // 6 ci steps, operands double-buffered: step k+1's LDS reads are issued before
+      // step k's MFMAs
+      auto ld = [&](int k0, bf16x8 (&a)[NPT], bf16x8 (&b)[3]) {
 #pragma unroll
         for (int ct = 0; ct < 3; ++ct)
           b[ct] = *reinterpret_cast<const bf16x8*>(&sW[(ct * 32 + l32) * DCP + k0 + 8 * hh]);
 #pragma unroll
-        for (int t = 0; t < NPT; ++t) {
-          const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sD[aoff[t] + k0]);
+        for (int t = 0; t < NPT; ++t) a[t] = *reinterpret_cast<const bf16x8*>(&sD[aoff[t] + k0]);
+      };
+      auto mm = [&](const bf16x8 (&a)[NPT], const bf16x8 (&b)[3]) {
 #pragma unroll
-          for (int ct = 0; ct < 3; ++ct) acc[t][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[ct], acc[t][ct], 0, 0, 0);
+        for (int t = 0; t < NPT; ++t)
+#pragma unroll
+          for (int ct = 0; ct < 3; ++ct) acc[t][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t], b[ct], acc[t][ct], 0, 0, 0);
+      };
+      bf16x8 a0[NPT], b0[3], a1[NPT], b1[3];
+      ld(0, a0, b0);
+      __builtin_amdgcn_sched_group_barrier(0x100, NPT + 3, 0);  // pinned order: reads(k+1), MFMAs(k)
+#pragma unroll
+      for (int k0 = 0; k0 < COUT; k0 += 32) {
+        ld(k0 + 16, a1, b1);
+        __builtin_amdgcn_sched_group_barrier(0x100, NPT + 3, 0);
+        mm(a0, b0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 3 * NPT, 0);
+        if (k0 + 32 < COUT) {
+          ld(k0 + 32, a0, b0);
+          __builtin_amdgcn_sched_group_barrier(0x100, NPT + 3, 0);
         }
+        mm(a1, b1);
+        __builtin_amdgcn_sched_group_barrier(0x008, 3 * NPT, 0);
       }
       __syncthreads();  // sW (and, after the last tap, sD) fully read
       if (tap + 1 < 9) {

@@ -314,18 +314,32 @@ __global__ __launch_bounds__(256, PF ? 1 : (NPT <= 2 ? 2 : 1)) void k_conv_gn_fw
             for (int ct = 0; ct < 3; ++ct)
               acc[t][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq[ks][t], bq[ks][ct], acc[t][ct], 0, 0, 0);
       } else {
-#pragma unroll
-        for (int k0 = 0; k0 < CIN; k0 += 16) {
-          bf16x8 b[3];
+        // k steps with double-buffered operands, order pinned: step k+1's LDS reads are
+        // issued before step k's MFMAs (left alone, the scheduler reuses one operand set
+        // and waits on every read)
+        constexpr int KS = CIN / 16;
+        bf16x8 A[2][NPT], B[2][3];
+        auto ld = [&](int ks, bf16x8 (&a)[NPT], bf16x8 (&b)[3]) {
 #pragma unroll
           for (int ct = 0; ct < 3; ++ct)
-            b[ct] = *reinterpret_cast<const bf16x8*>(&sWt[(ct * 32 + l32) * CINP + k0 + 8 * hh]);
+            b[ct] = *reinterpret_cast<const bf16x8*>(&sWt[(ct * 32 + l32) * CINP + ks * 16 + 8 * hh]);
 #pragma unroll
-          for (int t = 0; t < NPT; ++t) {
-            const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sX[aoff[t] + k0]);
+          for (int t = 0; t < NPT; ++t) a[t] = *reinterpret_cast<const bf16x8*>(&sX[aoff[t] + ks * 16]);
+        };
+        ld(0, A[0], B[0]);
+        __builtin_amdgcn_sched_group_barrier(0x100, NPT + 3, 0);
 #pragma unroll
-            for (int ct = 0; ct < 3; ++ct) acc[t][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[ct], acc[t][ct], 0, 0, 0);
+        for (int ks = 0; ks < KS; ++ks) {
+          if (ks + 1 < KS) {
+            ld(ks + 1, A[(ks + 1) & 1], B[(ks + 1) & 1]);
+            __builtin_amdgcn_sched_group_barrier(0x100, NPT + 3, 0);
           }
+#pragma unroll
+          for (int t = 0; t < NPT; ++t)
+#pragma unroll
+            for (int ct = 0; ct < 3; ++ct)
+              acc[t][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[ks & 1][t], B[ks & 1][ct], acc[t][ct], 0, 0, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 3 * NPT, 0);
         }
       }
       if (GL) {

@@ -170,9 +170,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
             s2[j] += zf * yh;
             s3[j] += yh;
           }
-          const u32x4 zv = __builtin_bit_cast(u32x4, z8);
-          *reinterpret_cast<u32x4*>(&sD[px * DCP + c8 * 8]) = zv;
-          if (p.dz) *reinterpret_cast<u32x4*>(&p.dz[((size_t)n * P + px) * COUT + c8 * 8]) = zv;
+          *reinterpret_cast<u32x4*>(&sD[px * DCP + c8 * 8]) = __builtin_bit_cast(u32x4, z8);
         }
       }
     }
@@ -236,7 +234,11 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
       for (int i = 0; i < NCH; ++i) {
         const int px = pg + PG * i;
         if (px < P) {
-          const bf16x8 z8 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(&sD[px * DCP + c8 * 8]));
+          const u32x4 zv = *reinterpret_cast<const u32x4*>(&sD[px * DCP + c8 * 8]);
+          // dz is stored here rather than in pass 1: a store there would sit between the
+          // next chunk batch's loads and their use, and vmcnt would drain it each batch
+          if (p.dz) *reinterpret_cast<u32x4*>(&p.dz[((size_t)n * P + px) * COUT + c8 * 8]) = zv;
+          const bf16x8 z8 = __builtin_bit_cast(bf16x8, zv);
           const bf16x8 y8 = __builtin_bit_cast(bf16x8, yr[i]);
           bf16x8 d8;
 #pragma unroll

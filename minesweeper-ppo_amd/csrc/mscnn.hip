@@ -141,7 +141,7 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds_dst) {
     const u32x4* xs_ = reinterpret_cast<const u32x4*>(p.x + (size_t)(n_) * P * CIN);   \
     _Pragma("unroll") for (int k_ = 0; k_ < NPF; ++k_) {                                \
       const int i_ = tid + 256 * k_;                                                    \
-      if (i_ < P * C8) v_[k_] = xs_[i_];                                                \
+      if ((FULL && k_ < C8) || i_ < P * C8) v_[k_] = xs_[i_]; /* FULL: P = 256 */      \
     }                                                                                   \
   } while (0)
 #define MC_LOAD_W(tap_, v_)                                                             \
@@ -149,7 +149,7 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds_dst) {
     const u32x4* ws_ = reinterpret_cast<const u32x4*>(p.wt + (size_t)(tap_) * COUT * CIN); \
     _Pragma("unroll") for (int k_ = 0; k_ < NWC; ++k_) {                                \
       const int i_ = tid + 256 * k_;                                                    \
-      if (i_ < COUT * C8) v_[k_] = ws_[i_];                                             \
+      if (k_ < COUT * C8 / 256 || i_ < COUT * C8) v_[k_] = ws_[i_]; /* static: full */ \
     }                                                                                   \
   } while (0)
 #define MC_STORE_W(buf_, v_)                                                            \
@@ -157,7 +157,7 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds_dst) {
     __bf16* d_ = sW + (buf_) * COUT * CINP;                                             \
     _Pragma("unroll") for (int k_ = 0; k_ < NWC; ++k_) {                                \
       const int i_ = tid + 256 * k_;                                                    \
-      if (i_ < COUT * C8) {                                                             \
+      if (k_ < COUT * C8 / 256 || i_ < COUT * C8) {                                    \
         const int co_ = i_ / C8, c8_ = i_ - co_ * C8;                                   \
         *reinterpret_cast<u32x4*>(&d_[co_ * CINP + c8_ * 8]) = v_[k_];                  \
       }                                                                                 \
@@ -242,7 +242,7 @@ __global__ __launch_bounds__(256, PF ? 1 : (NPT <= 2 ? 2 : 1)) void k_conv_gn_fw
 #pragma unroll
     for (int k = 0; k < NPF; ++k) {
       const int i = tid + 256 * k;
-      if (i < P * C8) {
+      if ((FULL && k < C8) || i < P * C8) {  // FULL: P = 256, every chunk in range
         const int px = i / C8, c8 = i - px * C8;
         *reinterpret_cast<u32x4*>(&sX[px * CINP + c8 * 8]) = xin[k];
       }

@@ -222,7 +222,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
 #pragma unroll
       for (int k = 0; k < NWC; ++k) {
         const int c = tid + 256 * k;
-        if (c < COUT * NC8) wr[k] = reinterpret_cast<const u32x4*>(p.wT)[c];
+        if (k < COUT * NC8 / 256 || c < COUT * NC8) wr[k] = reinterpret_cast<const u32x4*>(p.wT)[c];
       }
     }
     if (gact) {
@@ -256,7 +256,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
 #pragma unroll
     for (int k = 0; k < NWC; ++k) {
       const int c = tid + 256 * k;
-      if (c < COUT * NC8) {
+      if (k < COUT * NC8 / 256 || c < COUT * NC8) {
         const int ci = c / NC8, k8 = c - ci * NC8;
         *reinterpret_cast<u32x4*>(&sW[ci * DCP + k8 * 8]) = wr[k];
       }
@@ -281,7 +281,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
 #pragma unroll
         for (int k = 0; k < NWC; ++k) {
           const int c = tid + 256 * k;
-          if (c < COUT * NC8) wr[k] = ws[c];
+          if (k < COUT * NC8 / 256 || c < COUT * NC8) wr[k] = ws[c];  // the first 4 chunks are always full
         }
       }
       const int dr = tap / 3 - 1, dc = tap % 3 - 1;
@@ -328,7 +328,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
 #pragma unroll
         for (int k = 0; k < NWC; ++k) {
           const int c = tid + 256 * k;
-          if (c < COUT * NC8) {
+          if (k < COUT * NC8 / 256 || c < COUT * NC8) {
             const int ci = c / NC8, k8 = c - ci * NC8;
             *reinterpret_cast<u32x4*>(&sW[ci * DCP + k8 * 8]) = wr[k];
           }

@@ -477,17 +477,29 @@ __global__ __launch_bounds__(256, PF ? 1 : (NPT <= 2 ? 2 : 1)) void k_conv_gn_fw
         cd[j3][j] = sAB[2 * COUT + cg * 8 + j];
       }
     }
+    // residual chunks are loaded RB at a time, all of a batch before its first store: a
+    // load issued after a store waits for that store too (vmcnt counts both), so one
+    // load per chunk would drain the stores once per chunk
+    constexpr int RB = (NEC + 1) / 2;
+    u32x4 rq[RB];
 #pragma unroll
     for (int k = 0; k < NEC; ++k) {
       const int c = tid + 256 * k;
-      if (c < P * (COUT / 8)) {
+      if (!PF && k % RB == 0) {
+#pragma unroll
+        for (int u = 0; u < RB; ++u) {
+          const int cu = tid + 256 * (k + u);
+          rq[u] = u32x4{0u, 0u, 0u, 0u};
+          if (p.res && k + u < NEC && ((FULL && k + u < NEC) || cu < P * (COUT / 8)))
+            rq[u] = *reinterpret_cast<const u32x4*>(&p.res[(size_t)n * P * COUT + (size_t)cu * 8]);
+        }
+      }
+      if ((FULL && k < NEC) || c < P * (COUT / 8)) {
         const size_t o = (size_t)n * P * COUT + (size_t)c * 8;
         const u32x4 yv = *reinterpret_cast<const u32x4*>(&sO[c * 8]);
         if (p.ysave) *reinterpret_cast<u32x4*>(&p.ysave[o]) = yv;
         const bf16x8 y8 = __builtin_bit_cast(bf16x8, yv);
-        bf16x8 r8 = bf16x8{};
-        if (PF) r8 = __builtin_bit_cast(bf16x8, rv[PF ? k : 0]);
-        else if (p.res) r8 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(&p.res[o]));
+        const bf16x8 r8 = __builtin_bit_cast(bf16x8, PF ? rv[PF ? k : 0] : rq[k % RB]);
         bf16x8 o8;
         uint32_t mb = 0u;
 #pragma unroll

@@ -75,7 +75,8 @@ __host__ __device__ constexpr int red_bytes() {  // sRed [PG][3][96] f32, aliase
 }
 __host__ __device__ inline int bwd_data_lds(int P) { return dtile_bytes(P) + red_bytes() + 6 * COUT * 4; }
 
-template <int NPT, bool DGRAD, int NCH>
+// RM: the ReLU decisions come from the forward's bitmask (p.rmask), else from out
+template <int NPT, bool DGRAD, int NCH, bool RM>
 __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int H = p.H, W = p.W, P = H * W;
@@ -123,7 +124,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
     float s1[8], s2[8], s3[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) s1[j] = s2[j] = s3[j] = 0.f;
-    constexpr int LB = 4;  // chunks whose loads are in flight together
+    constexpr int LB = RM ? 7 : 4;  // chunks whose loads are in flight together
 #pragma unroll
     for (int i0 = 0; i0 < NCH; i0 += LB) {
       u32x4 dv[LB], ov[LB];
@@ -137,7 +138,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
           const size_t o = ((size_t)n * P + px) * COUT + c8 * 8;
 #ifndef MC_EXP_B_NO_P1LOAD
           dv[u] = *reinterpret_cast<const u32x4*>(&p.dout[o]);
-          if (p.rmask) mv[u] = p.rmask[((size_t)n * P + px) * NC8 + c8];
+          if (RM) mv[u] = p.rmask[((size_t)n * P + px) * NC8 + c8];
           else ov[u] = *reinterpret_cast<const u32x4*>(&p.out[o]);
           yr[i] = *reinterpret_cast<const u32x4*>(&p.y[o]);
 #else
@@ -154,7 +155,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
           const bf16x8 d8 = __builtin_bit_cast(bf16x8, dv[u]);
           const bf16x8 y8 = __builtin_bit_cast(bf16x8, yr[i]);
           uint32_t pos = mv[u];
-          if (!p.rmask) {  // (uniform)
+          if (!RM) {
             const bf16x8 o8 = __builtin_bit_cast(bf16x8, ov[u]);
 #pragma unroll
             for (int j = 0; j < 8; ++j) pos |= ((float)o8[j] > 0.f ? 1u : 0u) << j;
@@ -621,14 +622,20 @@ void set_lds_attr(K kernel) {
   (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
-template <int NPT, bool DGRAD, int NCH>
-void launch_bwd_data(const BwdDataParams& p, int grid, size_t lds, hipStream_t s) {
+template <int NPT, bool DGRAD, int NCH, bool RM>
+void launch_bwd_data_t(const BwdDataParams& p, int grid, size_t lds, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    set_lds_attr(k_bwd_data<NPT, DGRAD, NCH>);
+    set_lds_attr(k_bwd_data<NPT, DGRAD, NCH, RM>);
     attr = true;
   }
-  hipLaunchKernelGGL((k_bwd_data<NPT, DGRAD, NCH>), dim3(grid), dim3(256), lds, s, p);
+  hipLaunchKernelGGL((k_bwd_data<NPT, DGRAD, NCH, RM>), dim3(grid), dim3(256), lds, s, p);
+}
+
+template <int NPT, bool DGRAD, int NCH>
+void launch_bwd_data(const BwdDataParams& p, int grid, size_t lds, hipStream_t s) {
+  if (p.rmask) launch_bwd_data_t<NPT, DGRAD, NCH, true>(p, grid, lds, s);
+  else launch_bwd_data_t<NPT, DGRAD, NCH, false>(p, grid, lds, s);
 }
 
 template <bool DGRAD>

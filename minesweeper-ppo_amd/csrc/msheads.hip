@@ -196,18 +196,31 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams& p, HeadLds& 
     }
 #else
     // (prefetching the next tile here needs ~26 more VGPRs than the kernel has: spills)
+    // every load is issued unconditionally from a clamped row and masked afterwards:
+    // a guarded load sits in its own exec branch with its own vmcnt(0), one round
+    // trip per chunk
+    {
+      u32x4 v[NFC];
 #pragma unroll
-    for (int i = 0; i < NFC; ++i) {
-      const int c = tid + 256 * i + zo, r = c / 12, ch = c - r * 12;
-      const int64_t row = base + r;
-      u32x4 v = u32x4{0u, 0u, 0u, 0u};
-      if (row < p.M) v = *reinterpret_cast<const u32x4*>(&p.f[row * C + ch * 8]);
-      *reinterpret_cast<u32x4*>(&L.f[sf_off(r, ch * 8)]) = v;
-    }
-    if (tid < TR) {
-      const int64_t row = base + tid;
-      L.dl[0][tid] = row < p.M ? p.dlp[row] : 0.f;
-      L.dl[1][tid] = (row < p.M && p.dlm) ? p.dlm[row] : 0.f;
+      for (int i = 0; i < NFC; ++i) {
+        const int c = tid + 256 * i + zo, r = c / 12, ch = c - r * 12;
+        const int64_t row = base + r < p.M ? base + r : p.M - 1;
+        v[i] = *reinterpret_cast<const u32x4*>(&p.f[row * C + ch * 8]);
+      }
+      const int64_t rowd = base + (tid & (TR - 1)) < p.M ? base + (tid & (TR - 1)) : p.M - 1;
+      const float d0 = p.dlp[rowd];
+      const float d1 = p.dlm ? p.dlm[rowd] : 0.f;
+#pragma unroll
+      for (int i = 0; i < NFC; ++i) {
+        const int c = tid + 256 * i + zo, r = c / 12, ch = c - r * 12;
+        if (base + r >= p.M) v[i] = u32x4{0u, 0u, 0u, 0u};
+        *reinterpret_cast<u32x4*>(&L.f[sf_off(r, ch * 8)]) = v[i];
+      }
+      if (tid < TR) {
+        const bool ok = base + tid < p.M;
+        L.dl[0][tid] = ok ? d0 : 0.f;
+        L.dl[1][tid] = ok ? d1 : 0.f;
+      }
     }
 #endif
     __syncthreads();
@@ -252,11 +265,27 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams& p, HeadLds& 
     // ---- df^T[k][px] = sum_c W1p^T[k][c] dh[px][c] (policy channels only) ----
     {
       f32x16 acc2[3];
-#pragma unroll
-      for (int kt = 0; kt < 3; ++kt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc2[kt][i] = 0.f;
       const int rb = wave * 32 + l32 + zo;
+      const int64_t row = base + rb;
+      if (p.gadd) {  // (uniform) the accumulators start at gadd[m / P]: 12 loads issued
+                     // together, ahead of the MFMAs (rows past M read row M-1, discarded)
+        const float* ga = p.gadd + ((row < p.M ? row : p.M - 1) / p.P) * C;
+#pragma unroll
+        for (int kt = 0; kt < 3; ++kt)
+#pragma unroll
+          for (int gg = 0; gg < 4; ++gg) {
+            const float4 a4 = *reinterpret_cast<const float4*>(&ga[kt * 32 + 8 * gg + 4 * hh]);
+            acc2[kt][4 * gg + 0] = a4.x;
+            acc2[kt][4 * gg + 1] = a4.y;
+            acc2[kt][4 * gg + 2] = a4.z;
+            acc2[kt][4 * gg + 3] = a4.w;
+          }
+      } else {
+#pragma unroll
+        for (int kt = 0; kt < 3; ++kt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) acc2[kt][i] = 0.f;
+      }
 #pragma unroll
       for (int ks = 0; ks < 6; ++ks) {
         const bf16x8 b = *reinterpret_cast<const bf16x8*>(&L.dh[sd_off(rb, ks * 16 + 8 * hh)]);
@@ -269,8 +298,6 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams& p, HeadLds& 
       // acc2[kt][r] = df[px = wave*32 + l32][k = kt*32 + 8*(r>>2) + 4*hh + (r&3)]:
       // 8-B pieces of 64 different rows; staged in this wave's 32 rows of L.df, then
       // written as contiguous 16-B chunks (the wave's rows are 6 KiB of contiguous df)
-      const int64_t row = base + rb;
-      const float* ga = (p.gadd && row < p.M) ? p.gadd + (row / p.P) * C : nullptr;
 #pragma unroll
       for (int kt = 0; kt < 3; ++kt)
 #pragma unroll
@@ -279,13 +306,6 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams& p, HeadLds& 
           float v[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[j] = acc2[kt][4 * gg + j];
-          if (ga) {
-            const float4 a4 = *reinterpret_cast<const float4*>(&ga[k0]);
-            v[0] += a4.x;
-            v[1] += a4.y;
-            v[2] += a4.z;
-            v[3] += a4.w;
-          }
           *reinterpret_cast<bf16x4*>(&L.df[rb * C + k0]) =
               bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
         }

@@ -69,25 +69,38 @@ __global__ __launch_bounds__(256, 2) void k_heads_fwd(HeadFwdParams p) {
     const int zo = opaque0();
     const int64_t row = tile * TR + wave * 32 + l32;
     const bool valid = row < p.M;
+    // f rows: unconditional loads from a clamped row (a guarded load sits in its own exec
+    // branch); rows past M are computed and not stored
+    const int64_t rowc = valid ? row : p.M - 1;
     bf16x8 b[6];
 #pragma unroll
-    for (int ks = 0; ks < 6; ++ks) {
-      u32x4 v = u32x4{0u, 0u, 0u, 0u};
-      if (valid) v = *reinterpret_cast<const u32x4*>(&p.f[row * C + ks * 16 + 8 * hh]);
-      b[ks] = __builtin_bit_cast(bf16x8, v);
-    }
+    for (int ks = 0; ks < 6; ++ks)
+      b[ks] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(&p.f[rowc * C + ks * 16 + 8 * hh]));
     f32x16 acc[NT];
 #pragma unroll
     for (int ct = 0; ct < NT; ++ct)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[ct][i] = 0.f;
+    // W1 operands double-buffered across k steps, order pinned (reads of k+1, MFMAs of k)
+    bf16x8 A[2][NT];
+    auto ld = [&](int ks, bf16x8 (&a)[NT]) {
 #pragma unroll
-    for (int ks = 0; ks < 6; ++ks)
+      for (int ct = 0; ct < NT; ++ct)
+        a[ct] = *reinterpret_cast<const bf16x8*>(&sW[(ct * 32 + l32) * WP + ks * 16 + 8 * hh + zo]);
+    };
+    ld(0, A[0]);
+    __builtin_amdgcn_sched_group_barrier(0x020, 6, 0);  // the six f loads first, together
+    __builtin_amdgcn_sched_group_barrier(0x100, NT, 0);
 #pragma unroll
-      for (int ct = 0; ct < NT; ++ct) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sW[(ct * 32 + l32) * WP + ks * 16 + 8 * hh + zo]);
-        acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[ks], acc[ct], 0, 0, 0);
+    for (int ks = 0; ks < 6; ++ks) {
+      if (ks + 1 < 6) {
+        ld(ks + 1, A[(ks + 1) & 1]);
+        __builtin_amdgcn_sched_group_barrier(0x100, NT, 0);
       }
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[ks & 1][ct], b[ks], acc[ct], 0, 0, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, NT, 0);
+    }
     // acc[ct][r] = H^T[c = ct*32 + 8*(r>>2) + 4*hh + (r&3)][px = l32]
     float s[2] = {0.f, 0.f};
 #pragma unroll
@@ -95,8 +108,10 @@ __global__ __launch_bounds__(256, 2) void k_heads_fwd(HeadFwdParams p) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int c0 = ct * 32 + 8 * g + 4 * hh;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) s[ct / 3] += fmaxf(acc[ct][4 * g + j] + sB1[c0 + j + zo], 0.f) * sW2[c0 + j + zo];
+        const float4 bb = *reinterpret_cast<const float4*>(&sB1[c0 + zo]);
+        const float4 ww = *reinterpret_cast<const float4*>(&sW2[c0 + zo]);
+        s[ct / 3] += fmaxf(acc[ct][4 * g + 0] + bb.x, 0.f) * ww.x + fmaxf(acc[ct][4 * g + 1] + bb.y, 0.f) * ww.y +
+                     fmaxf(acc[ct][4 * g + 2] + bb.z, 0.f) * ww.z + fmaxf(acc[ct][4 * g + 3] + bb.w, 0.f) * ww.w;
       }
     s[0] += __shfl_xor(s[0], 32);
     if (MINE) s[1] += __shfl_xor(s[1], 32);

@@ -175,6 +175,16 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
         }
       }
     }
+    // tap 0's W^T: loaded here, its latency hidden behind the channel reductions
+    constexpr int NWC = (COUT * NC8 + 255) / 256;  // 16-B chunks of one W^T tap per thread
+    u32x4 wr[NWC];
+    if (DGRAD) {
+#pragma unroll
+      for (int k = 0; k < NWC; ++k) {
+        const int c = tid + 256 * k;
+        if (k < COUT * NC8 / 256 || c < COUT * NC8) wr[k] = reinterpret_cast<const u32x4*>(p.wT)[c];
+      }
+    }
     if (gact) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -216,16 +226,19 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
     }
     __syncthreads();
 
-    // ---------------- pass 2: dy (GroupNorm backward) -> LDS tile + HBM ----------------
-    constexpr int NWC = (COUT * NC8 + 255) / 256;  // 16-B chunks of one W^T tap per thread
-    u32x4 wr[NWC];
+    // tap 0's W^T goes to sW (free now: the sums are read) before pass 2 issues its
+    // stores: a load consumed behind those stores would wait for all of them
     if (DGRAD) {
 #pragma unroll
       for (int k = 0; k < NWC; ++k) {
         const int c = tid + 256 * k;
-        if (k < COUT * NC8 / 256 || c < COUT * NC8) wr[k] = reinterpret_cast<const u32x4*>(p.wT)[c];
+        if (k < COUT * NC8 / 256 || c < COUT * NC8) {
+          const int ci = c / NC8, k8 = c - ci * NC8;
+          *reinterpret_cast<u32x4*>(&sW[ci * DCP + k8 * 8]) = wr[k];
+        }
       }
     }
+    // ---------------- pass 2: dy (GroupNorm backward) -> LDS tile + HBM ----------------
     if (gact) {
       float A[8];
 #pragma unroll
@@ -253,15 +266,6 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
       }
     }
     if (!DGRAD) continue;  // (uniform) the stem's input needs no gradient
-
-#pragma unroll
-    for (int k = 0; k < NWC; ++k) {
-      const int c = tid + 256 * k;
-      if (k < COUT * NC8 / 256 || c < COUT * NC8) {
-        const int ci = c / NC8, k8 = c - ci * NC8;
-        *reinterpret_cast<u32x4*>(&sW[ci * DCP + k8 * 8]) = wr[k];
-      }
-    }
     __syncthreads();
 
     // ---------------- dgrad: dx = sum_tap shift(dy) . W^T[tap] ----------------

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MSENV_ABI_VERSION 1
+#define MSENV_ABI_VERSION 2
 
 enum {
   MS_OK = 0,
@@ -166,11 +166,14 @@ int ms_gae(const float* rewards, const float* values, const uint8_t* dones,
 /* Replaces masked_fill + Categorical(logits).sample/log_prob
  * (train_rl.py:229-235). logits f32[N,A], mask u8[N,A] (rows with no valid
  * cell are treated as all-valid, train_rl.py:166-168). Gumbel-max sampling
- * from a counter-based hash of (seed, counter, row, cell); writes actions
- * int64[N] and logp f32[N] (log_softmax of the masked row at the action). */
+ * from a counter-based hash of (seed, counter, row_begin + row, cell): with
+ * row_begin = the shard's first GLOBAL env index, a sharded rollout draws the
+ * same actions as an unsharded one. Writes actions int64[N] and logp f32[N]
+ * (log_softmax of the masked row at the action). */
 int ms_sample_masked(const float* logits, const uint8_t* mask, int64_t N,
-                     int32_t A, uint64_t seed, uint64_t counter,
-                     int64_t* actions, float* logp, void* stream);
+                     int32_t A, int64_t row_begin, uint64_t seed,
+                     uint64_t counter, int64_t* actions, float* logp,
+                     void* stream);
 
 #ifdef __cplusplus
 }

@@ -1326,8 +1326,9 @@ __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t counter, uint
 }
 
 __global__ __launch_bounds__(256) void k_sample(const float* __restrict__ logits, const uint8_t* __restrict__ mask,
-                                                int64_t N, int A, uint64_t seed, uint64_t counter,
-                                                int64_t* __restrict__ actions, float* __restrict__ logp) {
+                                                int64_t N, int A, int64_t row_begin, uint64_t seed,
+                                                uint64_t counter, int64_t* __restrict__ actions,
+                                                float* __restrict__ logp) {
   const int lane = lane_id();
   const int64_t row = (int64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
   if (row >= N) return;
@@ -1348,7 +1349,7 @@ __global__ __launch_bounds__(256) void k_sample(const float* __restrict__ logits
     if (all_valid || mr[i]) {
       const float l = lr[i];
       se += expf(l - mx);
-      const float u = uniform01(seed, counter, (uint64_t)row, (uint64_t)i);
+      const float u = uniform01(seed, counter, (uint64_t)(row_begin + row), (uint64_t)i);
       const float gk = l - logf(-logf(u));
       if (gk > best || (gk == best && i < best_i)) {
         best = gk;
@@ -1855,11 +1856,12 @@ int ms_gae(const float* rewards, const float* values, const uint8_t* dones, cons
   return e == hipSuccess ? MS_OK : hip_fail(e, "ms_gae launch");
 }
 
-int ms_sample_masked(const float* logits, const uint8_t* mask, int64_t N, int32_t A, uint64_t seed,
-                     uint64_t counter, int64_t* actions, float* logp, void* stream) {
-  if (!logits || !mask || !actions || !logp || N <= 0 || A <= 0) return fail(MS_EINVAL, "ms_sample_masked: bad argument");
+int ms_sample_masked(const float* logits, const uint8_t* mask, int64_t N, int32_t A, int64_t row_begin,
+                     uint64_t seed, uint64_t counter, int64_t* actions, float* logp, void* stream) {
+  if (!logits || !mask || !actions || !logp || N <= 0 || A <= 0 || row_begin < 0)
+    return fail(MS_EINVAL, "ms_sample_masked: bad argument");
   hipLaunchKernelGGL(k_sample, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, (hipStream_t)stream, logits, mask, N,
-                     (int)A, seed, counter, actions, logp);
+                     (int)A, row_begin, seed, counter, actions, logp);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? MS_OK : hip_fail(e, "ms_sample_masked launch");
 }

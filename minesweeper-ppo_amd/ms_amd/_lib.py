@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # MSENV_LIB may point at libmsenv_diag.so (tools/diag_step.py); default is the product build
 LIB_PATH = os.environ.get("MSENV_LIB") or os.path.join(PKG_DIR, "libmsenv.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 MS_OUTCOME_NONE, MS_OUTCOME_WIN, MS_OUTCOME_LOSS = 0, 1, 2
 MS_TAPE_UNIFORM, MS_TAPE_SAFE_BIASED = 0, 1
@@ -52,7 +52,7 @@ SIGNATURES = {
     "ms_tape_actions": [_vp, _u64, _i32, _vp, _vp],
     "ms_run_tape": [_vp, _u64, _i32, _i32, _i32] + [_vp] * 10,
     "ms_gae": [_vp, _vp, _vp, _vp, _i32, _i64, _f32, _f32, _vp, _vp, _vp],
-    "ms_sample_masked": [_vp, _vp, _i64, _i32, _u64, _u64, _vp, _vp, _vp],
+    "ms_sample_masked": [_vp, _vp, _i64, _i32, _i64, _u64, _u64, _vp, _vp, _vp],
     "ms_set_late_start": [_vp, ctypes.c_double, _i32, _i32, _i32, _i32, _u64],
     "ms_late_rng_state": [_vp, _vp],
     # msenv_debug.h

@@ -115,15 +115,51 @@ class RolloutBuffer:
         B = self.obs.shape[0]
         idx = torch.randperm(B, device=self.device, generator=generator)
         for s in range(0, B, batch_size):
-            sel = idx[s:s + batch_size]
-            kw = dict(obs=self.obs[sel], action_mask=self.action_mask[sel], actions=self.actions[sel],
-                      old_logp=self.logp[sel], rewards=self.rewards[sel], dones=self.dones[sel],
-                      values=self.values[sel], advantages=self.advantages[sel], returns=self.returns[sel])
-            if self.mine_labels is not None:
-                kw["mine_labels"] = self.mine_labels[sel]
-                if self.mine_valid is not None:
-                    kw["mine_valid"] = self.mine_valid[sel]
-            yield Batch(**kw)
+            yield self._gather(idx[s:s + batch_size])
+
+    def get_stratified_minibatches(self, mini_batches: int, stripes: int, stripe_begin: int,
+                                   seed: int) -> Iterator[Batch]:
+        """World-invariant minibatches for data-parallel training. The GLOBAL env list is cut
+        into stripes of equal size; this buffer holds ``stripes`` of them, starting at global
+        stripe ``stripe_begin``. Each stripe's T*n_s rows get their own permutation, seeded by
+        (seed, global stripe), and minibatch k takes slice k of every stripe's permutation.
+        So minibatch k of a rank is exactly its part of minibatch k of an unsharded run with
+        the same seed, and all ranks hold equal row counts (the mean of the rank means is the
+        global mean). Compared with buffers.py:96-116's one randperm(B), every minibatch is
+        stratified over env stripes: it holds the same number of rows from each stripe."""
+        N, T = self.num_envs, self.steps
+        assert N % stripes == 0, "envs must split evenly into stripes"
+        n_s = N // stripes
+        rows_s = T * n_s
+        m_s = max(1, rows_s // mini_batches)
+        perms = []
+        for j in range(stripes):
+            g = torch.Generator(device=self.device)
+            g.manual_seed(_mix64(seed, stripe_begin + j))
+            q = torch.randperm(rows_s, device=self.device, generator=g)
+            perms.append((q // n_s) * N + j * n_s + (q % n_s))  # stripe row -> buffer row t*N + e
+        P = torch.stack(perms)
+        for s in range(0, rows_s, m_s):
+            yield self._gather(P[:, s:s + m_s].reshape(-1))
+
+    def _gather(self, sel: torch.Tensor) -> Batch:
+        kw = dict(obs=self.obs[sel], action_mask=self.action_mask[sel], actions=self.actions[sel],
+                  old_logp=self.logp[sel], rewards=self.rewards[sel], dones=self.dones[sel],
+                  values=self.values[sel], advantages=self.advantages[sel], returns=self.returns[sel])
+        if self.mine_labels is not None:
+            kw["mine_labels"] = self.mine_labels[sel]
+            if self.mine_valid is not None:
+                kw["mine_valid"] = self.mine_valid[sel]
+        return Batch(**kw)
+
+
+def _mix64(a: int, b: int) -> int:
+    """splitmix64 finaliser of (a, b) -> a 63-bit generator seed."""
+    M = (1 << 64) - 1
+    z = (a * 0x9E3779B97F4A7C15 + b + 0x632BE59BD9B4E019) & M
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+    return (z ^ (z >> 31)) >> 1
 
 
 __all__ = ["RolloutBuffer", "Batch"]

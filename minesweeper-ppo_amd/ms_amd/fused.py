@@ -11,6 +11,7 @@ import ctypes
 from typing import Optional, Tuple
 
 import torch
+from torch.utils.weak import WeakIdKeyDictionary
 
 from . import _lib as L
 
@@ -145,17 +146,21 @@ def conv_gn_bwd(dout: torch.Tensor, out: Optional[torch.Tensor], y: torch.Tensor
 # Whole-trunk fast path for CNNResidualPolicy (cnn_residual.py:30-96): stem + residual
 # blocks as fused layers, activations NHWC bf16, autograd through mc_conv_gn_bwd.
 
-_wcache: dict = {}
+# weight -> {kind: (version, packed)}; weak keys, so a dropped model frees its packed copies
+# (identity-keyed: tensor == is elementwise)
+_wcache = WeakIdKeyDictionary()
 
 
 def _packed(w: torch.Tensor, kind: str, cin_pad: int = 0) -> torch.Tensor:
     """bf16 re-layout of a conv weight, cached until the optimizer bumps its version."""
-    key = (id(w), kind)
-    hit = _wcache.get(key)
-    if hit is not None and hit[0] == w._version and hit[1] is w:
-        return hit[2]
+    ent = _wcache.get(w)
+    if ent is None:
+        ent = _wcache[w] = {}
+    hit = ent.get(kind)
+    if hit is not None and hit[0] == w._version:
+        return hit[1]
     t = prep_weight(w.detach(), cin_pad) if kind == "f" else prep_weight_t(w.detach())
-    _wcache[key] = (w._version, w, t)
+    ent[kind] = (w._version, t)
     return t
 
 
@@ -269,17 +274,20 @@ _hcache: dict = {}
 def _head_pack(pol, mine):
     """bf16 [192|96, 96] W1 (policy rows first), its policy transpose, f32 b1 / w2 / b2."""
     heads = [pol] + ([mine] if mine is not None else [])
-    key = tuple((id(m.weight), m.weight._version, id(m.bias), m.bias._version) for h in heads for m in (h[0], h[2]))
+    params = tuple(t for h in heads for m in (h[0], h[2]) for t in (m.weight, m.bias))
+    vers = tuple(t._version for t in params)
+    # the entry holds the parameters themselves and compares by identity: ids of freed
+    # parameters can be reused by a new model at the same versions
     hit = _hcache.get(len(heads))
-    if hit is not None and hit[0] == key:
-        return hit[1]
+    if hit is not None and hit[1] == vers and all(a is b for a, b in zip(hit[0], params)):
+        return hit[2]
     w1 = torch.cat([h[0].weight.detach().reshape(COUT, COUT) for h in heads]).to(torch.bfloat16).contiguous()
     w1pT = pol[0].weight.detach().reshape(COUT, COUT).t().to(torch.bfloat16).contiguous()
     b1 = torch.cat([h[0].bias.detach() for h in heads]).float().contiguous()
     w2 = torch.cat([h[2].weight.detach().reshape(COUT) for h in heads]).float().contiguous()
     b2 = torch.cat([h[2].bias.detach().reshape(1) for h in heads]).float().contiguous()
     packed = (w1, w1pT, b1, w2, b2)
-    _hcache[len(heads)] = (key, packed)
+    _hcache[len(heads)] = (params, vers, packed)
     return packed
 
 

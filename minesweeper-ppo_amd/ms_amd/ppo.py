@@ -40,14 +40,26 @@ class PPOConfig:
 class FlatGrads:
     """All parameter gradients as views of one contiguous buffer, so the
     data-parallel reduction is a single RCCL all-reduce (3.80 MB for the
-    shipped 950,947-parameter model) instead of one per tensor."""
+    shipped 950,947-parameter model) instead of one per tensor.
+
+    A post-accumulate hook records which parameters the backward reached.
+    ``release_unused()`` sets ``.grad = None`` on the others (e.g. the mine
+    head when both belief-loss weights are 0), so the optimizer skips them as
+    it does after the reference's ``zero_grad(set_to_none=True)``
+    (ppo.py:96): no weight decay, no momentum step on a stale gradient."""
 
     def __init__(self, params):
         self.params = [p for p in params if p.requires_grad]
         n = sum(p.numel() for p in self.params)
         dev = self.params[0].device
         self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.reached = set()
+        for p in self.params:
+            p.register_post_accumulate_grad_hook(self._mark)
         self.attach()
+
+    def _mark(self, p):
+        self.reached.add(id(p))
 
     def attach(self):
         o = 0
@@ -58,12 +70,21 @@ class FlatGrads:
 
     def zero(self):
         self.flat.zero_()
+        self.reached.clear()
         # an optimizer's zero_grad(set_to_none=True) or autograd may have replaced .grad
         for p in self.params:
             if p.grad is None or p.grad.data_ptr() < self.flat.data_ptr() or \
                     p.grad.data_ptr() >= self.flat.data_ptr() + self.flat.numel() * 4:
                 self.attach()
                 break
+
+    def release_unused(self):
+        """After backward: parameters no gradient reached get ``.grad = None``
+        (``zero()`` re-attaches the views). Which parameters are reached
+        depends only on the loss configuration, so it agrees across ranks."""
+        for p in self.params:
+            if id(p) not in self.reached:
+                p.grad = None
 
     def all_reduce_mean(self, group=None):
         dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
@@ -143,6 +164,8 @@ def ppo_update(model, optimizer, batch, cfg: PPOConfig, scaler=None, *,
         optimizer.zero_grad(set_to_none=True)
     if scaler is not None and batch.obs.is_cuda:
         scaler.scale(loss).backward()
+        if flat_grads is not None:
+            flat_grads.release_unused()
         if group is not None:
             flat_grads.all_reduce_mean(group)
         scaler.unscale_(optimizer)
@@ -151,6 +174,8 @@ def ppo_update(model, optimizer, batch, cfg: PPOConfig, scaler=None, *,
         scaler.update()
     else:
         loss.backward()
+        if flat_grads is not None:
+            flat_grads.release_unused()
         if group is not None:
             flat_grads.all_reduce_mean(group)
         torch.nn.utils.clip_grad_norm_(model.parameters(), cfg.max_grad_norm)

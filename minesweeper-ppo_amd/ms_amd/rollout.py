@@ -11,7 +11,9 @@ boundary three times per step, train_rl.py:198-199, 239, 246-247).
 Sampling is Gumbel-max over the valid cells from a counter-based hash, so the
 action distribution equals softmax(masked logits) (checked statistically in
 tests); the stream of random numbers is not torch's, hence rollouts are not
-bitwise those of torch.distributions.Categorical.
+bitwise those of torch.distributions.Categorical. The hash is keyed by the
+GLOBAL env index, so a rank's shard draws what the same envs draw in an
+unsharded run: rollouts do not depend on the world size.
 """
 from __future__ import annotations
 
@@ -27,9 +29,10 @@ from .env import OBS_CHANNELS, VecMinesweeper
 
 
 def sample_masked(logits: torch.Tensor, mask: torch.Tensor, seed: int, counter: int,
-                  actions: Optional[torch.Tensor] = None, logp: Optional[torch.Tensor] = None
-                  ) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Categorical(logits.masked_fill(~mask, -inf)).sample() + log_prob on device."""
+                  actions: Optional[torch.Tensor] = None, logp: Optional[torch.Tensor] = None,
+                  row_begin: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Categorical(logits.masked_fill(~mask, -inf)).sample() + log_prob on device. Row i draws
+    from the hash stream of global row ``row_begin + i``."""
     lib = L.load()
     lg = logits.detach().float().contiguous()
     n, a = lg.shape
@@ -38,7 +41,7 @@ def sample_masked(logits: torch.Tensor, mask: torch.Tensor, seed: int, counter: 
     if logp is None:
         logp = torch.empty(n, dtype=torch.float32, device=lg.device)
     m = mask.contiguous().view(torch.uint8)
-    L.check(lib.ms_sample_masked(L.ptr(lg), L.ptr(m), n, a, int(seed) & (2**64 - 1),
+    L.check(lib.ms_sample_masked(L.ptr(lg), L.ptr(m), n, a, int(row_begin), int(seed) & (2**64 - 1),
                                  int(counter) & (2**64 - 1), L.ptr(actions), L.ptr(logp),
                                  L.stream_ptr(lg.device)))
     return actions, logp
@@ -74,7 +77,8 @@ def collect_rollout(vec: VecMinesweeper, model: torch.nn.Module, steps: int, dev
             vec.mine_labels(s["mine_labels"], s["mine_valid"])
         with _autocast(device, amp_dtype):
             logits, values = model(s["obs"])
-        sample_masked(logits, s["action_mask"], sample_seed, sample_counter + t, s["actions"], s["logp"])
+        sample_masked(logits, s["action_mask"], sample_seed, sample_counter + t, s["actions"], s["logp"],
+                      row_begin=vec.env_begin)
         s["values"].copy_(values.float())
         if t + 1 < steps:
             nxt = buffer.slot(t + 1)

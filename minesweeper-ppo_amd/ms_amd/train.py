@@ -105,6 +105,37 @@ def aux_weight_at(update: int, total: int, base: float, warm_w: float, final_w: 
     return float(max(0.0, w))
 
 
+def _opt(training: Dict, key: str, conv, default, post=lambda v: v):
+    """One optional ``training:`` value, converted; a bad value keeps the default
+    (the try/except blocks of train_rl.py:456-504)."""
+    v = training.get(key)
+    if v is None:
+        return default
+    try:
+        return post(conv(v))
+    except Exception:
+        return default
+
+
+def aux_schedule_params(cfg: PPOTrainConfig, training: Dict):
+    """(base, warmup weight, final weight, warmup updates, decay power) as train_rl.py:456-504
+    reads them from the YAML ``training:`` section."""
+    training = training if isinstance(training, dict) else {}
+    base = float(getattr(cfg, "aux_mine_weight", 0.0))
+    warm_w = _opt(training, "aux_mine_warmup_weight", float, base)
+    final_w = _opt(training, "aux_mine_final_weight", float, base)
+    warm_u = _opt(training, "aux_mine_warmup_updates", int, 0, lambda v: max(0, v))
+    power = _opt(training, "aux_mine_decay_power", float, 1.0, lambda v: max(1e-6, v))
+    return base, warm_w, final_w, warm_u, power
+
+
+def early_stop_patience(training: Dict):
+    """train_rl.py:462-470: enabled only for an integer patience > 0."""
+    training = training if isinstance(training, dict) else {}
+    p = _opt(training, "early_stop_patience", int, None)
+    return p if p is not None and p > 0 else None
+
+
 class Trainer:
     """Holds env shard, model, optimizer and buffers; `update()` runs one PPO
     update. Used by main() and by bench.py's combined-loop measurement."""
@@ -149,15 +180,19 @@ class Trainer:
                                  aux_mine_calib_weight=cfg.aux_mine_calib_weight,
                                  max_grad_norm=cfg.max_grad_norm,
                                  beta_l2=float(training.get("beta_l2", 0.0)))
-        self.aux_base = float(cfg.aux_mine_weight)
-        self.aux_warm_w = float(training.get("aux_mine_warmup_weight", self.aux_base))
-        self.aux_final_w = float(training.get("aux_mine_final_weight", self.aux_base))
-        self.aux_warm_u = max(0, int(training.get("aux_mine_warmup_updates", 0)))
-        self.aux_power = max(1e-6, float(training.get("aux_mine_decay_power", 1.0)))
+        (self.aux_base, self.aux_warm_w, self.aux_final_w, self.aux_warm_u,
+         self.aux_power) = aux_schedule_params(cfg, training)
         self.buffer: RolloutBuffer | None = None
         self.seed = seed
-        self.gen = torch.Generator(device=self.device)
-        self.gen.manual_seed(seed * 1000003 + self.info.rank)
+        # minibatches are stratified over S stripes of the global env list (RolloutBuffer.
+        # get_stratified_minibatches): with S a multiple of the world size, rank r's minibatch k
+        # is its part of the unsharded run's minibatch k, so training does not depend on world
+        S = int(training.get("minibatch_strata", 8))
+        if S <= 0 or cfg.num_envs % S or S % self.info.world:
+            S = self.info.world
+        self.strata = S
+        self.stripes_local = S // self.info.world
+        self.stripe_begin = self.info.rank * self.stripes_local
 
     def update(self, update: int, profile: bool = False) -> Dict[str, float]:
         """One PPO update. ``profile`` synchronises between phases and adds
@@ -176,17 +211,17 @@ class Trainer:
         self.buffer, aux = collect_rollout(
             self.vec, self.model, cfg.steps_per_env, self.device, pc.aux_mine_weight,
             pc.aux_mine_calib_weight, amp_dtype=self.amp_dtype, buffer=self.buffer,
-            sample_seed=self.seed * 7919 + 17, sample_counter=(update << 20) + (self.info.rank << 40))
+            sample_seed=self.seed * 7919 + 17, sample_counter=update << 20)
         mark()
         self.buffer.compute_gae(aux["last_values"], gamma=cfg.gamma, lam=cfg.gae_lambda)
         mark()
-        B = self.vec.num_envs * cfg.steps_per_env
-        mb = B // cfg.mini_batches
         acc: Dict[str, torch.Tensor] = {}
         n = 0
         group = self.info.group if self.info.world > 1 else None
-        for _ in range(cfg.ppo_epochs):
-            for batch in self.buffer.get_minibatches(mb, generator=self.gen):
+        for epoch in range(cfg.ppo_epochs):
+            mbs = self.buffer.get_stratified_minibatches(cfg.mini_batches, self.stripes_local, self.stripe_begin,
+                                                         seed=(self.seed * 1000003 + update) * 64 + epoch)
+            for batch in mbs:
                 st = ppo_update(self.model, self.opt, batch, pc, self.scaler, amp_dtype=self.amp_dtype,
                                 group=group, flat_grads=self.flat, sync_stats=False)
                 for k, v in st.items():
@@ -278,8 +313,7 @@ def main(argv=None) -> None:
     if args.updates is not None:
         cfg.total_updates = int(args.updates)
     training = extras.get("training", {}) if isinstance(extras, dict) else {}
-    patience = training.get("early_stop_patience")
-    patience = int(patience) if patience is not None else None
+    patience = early_stop_patience(training)
     logging.basicConfig(level=logging.INFO if info.is_main else logging.WARNING,
                         format="[%(asctime)s] %(message)s", datefmt="%H:%M:%S")
     log = logging.getLogger("ms_amd.train")

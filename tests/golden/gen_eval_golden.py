@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.dirname(HERE))
 import eval as ref_eval  # noqa: E402  (the reference's eval.py, via PYTHONPATH)
 from minesweeper.env import EnvConfig  # noqa: E402
 
-from eval_model import DetModel  # noqa: E402
+from eval_model import DetModel, RuleModel  # noqa: E402
 
 rng = np.random.default_rng(7)
 d = {}
@@ -36,3 +36,13 @@ for (H, W, K, eps, ne) in ((8, 8, 4, 30, 7), (9, 9, 10, 24, 8), (16, 16, 40, 12,
     np.savez(os.path.join(HERE, f"eval_vec_{H}x{W}x{K}.npz"), keys=np.array(keys),
              values=np.array([res[k] for k in keys], dtype=np.float64), episodes=eps, num_envs=ne)
     print(H, W, K, {k: res[k] for k in ("win_rate", "avg_steps", "avg_progress", "belief_auroc", "belief_ece")})
+
+# RuleModel fixtures: enough episodes to include wins at 16x16x40 and at C5's 30x16x99, so
+# win accounting and the belief AUROC check run at the benchmark shapes
+for (H, W, K, eps, ne) in ((16, 16, 40, 96, 16), (30, 16, 99, 96, 16)):
+    m = RuleModel()
+    res = ref_eval.evaluate_vec(m, EnvConfig(H=H, W=W, mine_count=K), episodes=eps, seed=0, num_envs=ne)
+    keys = sorted(res)
+    np.savez(os.path.join(HERE, f"eval_vec_rule_{H}x{W}x{K}.npz"), keys=np.array(keys),
+             values=np.array([res[k] for k in keys], dtype=np.float64), episodes=eps, num_envs=ne)
+    print("rule", H, W, K, {k: res[k] for k in ("wins", "win_rate", "avg_steps", "belief_auroc", "belief_ece")})

@@ -19,6 +19,7 @@ Fixtures
   G5 model_*.npz      CNNResidualPolicy / CNNPolicy eval-mode fp32 outputs
                       (models/cnn_residual.py:30-96, models/cnn.py)
   G6 ppo.npz          one ppo_update on the small model (ppo.py:23-119)
+     ppo_full_16x16.npz one ppo_update on the shipped 96x5 model, with its gradients
 """
 from __future__ import annotations
 
@@ -191,6 +192,15 @@ def _sha(model):
     return h.hexdigest()
 
 
+def _sha_sd(npz_sd):
+    """sha256 over an _sd_to_npz dict (the initial weights are re-made by seeded init)."""
+    h = hashlib.sha256()
+    for k, v in npz_sd.items():
+        h.update(k[3:].encode())
+        h.update(np.ascontiguousarray(v).tobytes())
+    return h.hexdigest()
+
+
 def _rand_obs(n, H, W, seed):
     rng = np.random.default_rng(seed)
     obs = np.zeros((n, 10, H, W), np.float32)
@@ -266,7 +276,56 @@ def gen_ppo():
                         stat_values=np.array([stats[k] for k in sorted(stats)]), **init, **post)
 
 
+def gen_ppo_full():
+    """G6-full: one ppo_update of the SHIPPED model (96 ch x 5 blocks, seeded init at
+    manual_seed(0), dropout 0 so train mode is deterministic) on 64 16x16 samples, fp32,
+    no scaler. Also records the clipped gradients the optimizer stepped on."""
+    torch.set_float32_matmul_precision("highest")
+    torch.manual_seed(0)
+    H = W = 16
+    A = H * W
+    model = build_model("cnn_residual", obs_shape=(10, H, W),
+                        model_cfg=dict(stem_channels=96, blocks=5, dropout=0.0, value_hidden=256))
+    init = _sd_to_npz(model.state_dict())
+    opt = torch.optim.AdamW(model.parameters(), lr=3e-4)
+    grads = {}
+    step0 = opt.step
+
+    def step_and_record(*a, **k):
+        for n, p in model.named_parameters():
+            grads["grad::" + n] = p.grad.detach().numpy().copy()
+        return step0(*a, **k)
+    opt.step = step_and_record
+    B = 64
+    g = torch.Generator().manual_seed(13)
+    obs = torch.from_numpy(_rand_obs(B, H, W, 14))
+    mask = (obs[:, 0] == 0).reshape(B, A)
+    mask[:, 0] = True
+    actions = torch.multinomial(mask.float(), 1, generator=g).squeeze(1)
+    old_logp = -torch.rand(B, generator=g) * 3 - 4
+    values = torch.randn(B, generator=g) * 0.3
+    adv = torch.randn(B, generator=g)
+    rets = values + adv
+    labels = (torch.rand(B, H, W, generator=g) < 0.15).float()
+    valid = mask.reshape(B, H, W) & (torch.rand(B, H, W, generator=g) < 0.9)
+    batch = type("Batch", (), dict(obs=obs, action_mask=mask, actions=actions, old_logp=old_logp,
+                                   values=values, advantages=adv, returns=rets,
+                                   mine_labels=labels, mine_valid=valid))
+    cfg = PPOConfig(ent_coef=0.003, aux_mine_weight=0.05, aux_mine_calib_weight=0.01)
+    stats = ppo_update(model, opt, batch, cfg, scaler=None)
+    post = {"post::" + k: v.detach().numpy().copy() for k, v in model.state_dict().items()}
+    np.savez_compressed(os.path.join(HERE, "ppo_full_16x16.npz"), obs=obs.numpy(), mask=mask.numpy(),
+                        actions=actions.numpy(), old_logp=old_logp.numpy(), values=values.numpy(),
+                        advantages=adv.numpy(), returns=rets.numpy(), mine_labels=labels.numpy(),
+                        mine_valid=valid.numpy(), stat_names=np.array(sorted(stats)),
+                        stat_values=np.array([stats[k] for k in sorted(stats)]),
+                        init_sha256=np.bytes_(_sha_sd(init)), **grads, **post)
+
+
 def main():
+    if sys.argv[1:] == ["ppo_full"]:
+        gen_ppo_full()
+        return
     import minesweeper.env as E
     assert not E.HAS_ENV_NUMBA, "fixtures are defined against the BFS path; numba absent here"
     print("numpy", np.__version__, "torch", torch.__version__, file=sys.stderr)
@@ -282,6 +341,7 @@ def main():
     gen_gae()
     gen_model()
     gen_ppo()
+    gen_ppo_full()
 
 
 if __name__ == "__main__":

@@ -294,3 +294,42 @@ def test_run_tape_sharded_and_late_start(gpu):
     late.reset()
     with pytest.raises(MsEnvError):
         late.run_tape(0, 4, 0)
+
+
+@pytest.mark.parametrize("H,W,K,N", [(16, 16, 40, 4096), (9, 9, 10, 8192), (30, 16, 99, 8192), (16, 30, 99, 8192)],
+                         ids=["C2", "C3", "C5", "C5-transposed"])
+def test_full_size_configs_vs_oracle(gpu, H, W, K, N):
+    """BASELINE configs at their full env counts (C3 9x9x10 and C5 30x16x99 at N=8192 -- C5's
+    8 GPUs x 1024 envs is the same global env list), 20 steps of each tape: obs, mask, rewards,
+    dones, outcome, aux, labels, counts, mines and RNG state bit-exact with the C oracle."""
+    _diff_run(H, W, K, N=N, T=20, mode=0, seed=0, check_every=1)
+    _diff_run(H, W, K, N=N, T=20, mode=1, seed=1, check_every=4)
+
+
+def test_c4_eight_shards_equal_unsharded_32768(gpu):
+    """BASELINE C4 (16x16x40, N=32768 over 8 GPUs at 4096 each): the 8 shards of the global
+    env list, stepped side by side in one process, equal one unsharded 32768-env handle bit
+    for bit (obs, mask, rewards, dones, aux, RNG state), so the 8-GPU run is trajectory-
+    identical to a single device."""
+    from ms_amd import EnvConfig, VecMinesweeper
+    cfg = EnvConfig(H=16, W=16, mine_count=40)
+    N = 32768
+    full = VecMinesweeper(N, cfg, seed=0)
+    parts = [VecMinesweeper(N, cfg, seed=0, shard=(r, 8)) for r in range(8)]
+    assert all(p.num_envs == 4096 for p in parts)
+    full.reset()
+    for p in parts:
+        p.reset()
+    for t in range(20):
+        a = full.tape_actions(t, 1)
+        pa = [p.tape_actions(t, 1) for p in parts]
+        assert torch.equal(a, torch.cat(pa)), t
+        bf, rf, df, inf = full.step(a)
+        outs = [p.step(x) for p, x in zip(parts, pa)]
+        assert torch.equal(bf["obs"], torch.cat([o[0]["obs"] for o in outs])), t
+        assert torch.equal(bf["action_mask"], torch.cat([o[0]["action_mask"] for o in outs])), t
+        assert torch.equal(rf, torch.cat([o[1] for o in outs])), t
+        assert torch.equal(df, torch.cat([o[2] for o in outs])), t
+        for k in ("outcome", "step", "last_new_reveals", "revealed_frac"):
+            assert torch.equal(inf.tensors[k], torch.cat([o[3].tensors[k] for o in outs])), (t, k)
+    assert np.array_equal(full.rng_state(), np.concatenate([p.rng_state() for p in parts]))

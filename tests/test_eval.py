@@ -61,3 +61,39 @@ def test_evaluate_vec_matches_reference(gpu, board):
         assert got[k] == pytest.approx(ref[k], abs=1e-12), k
     assert got["belief_ece"] == pytest.approx(ref["belief_ece"], abs=1e-6)
     assert got["belief_auroc"] == pytest.approx(ref["belief_auroc"], abs=2e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("board", ["16x16x40", "30x16x99"])
+def test_evaluate_vec_rule_player_matches_reference(gpu, board):
+    """A rule player that wins (64/96 at 16x16x40, 2/96 at C5's 30x16x99): win accounting,
+    steps, progress and the belief AUROC / ECE at the benchmark shapes vs the reference."""
+    from eval_model import RuleModel
+    from ms_amd import EnvConfig
+    from ms_amd.eval import evaluate_vec
+    H, W, K = (int(v) for v in board.split("x"))
+    z = np.load(os.path.join(GOLDEN, f"eval_vec_rule_{board}.npz"))
+    ref = dict(zip([str(k) for k in z["keys"]], z["values"]))
+    assert ref["wins"] > 0
+    got = evaluate_vec(RuleModel().to(gpu), EnvConfig(H=H, W=W, mine_count=K), episodes=int(z["episodes"]),
+                       seed=0, num_envs=int(z["num_envs"]))
+    for k in ("win_rate", "win_ci_low", "win_ci_high", "avg_steps", "avg_progress", "invalid_rate", "wins",
+              "episodes"):
+        assert got[k] == pytest.approx(ref[k], abs=1e-12), k
+    assert got["belief_ece"] == pytest.approx(ref["belief_ece"], abs=1e-6)
+    assert got["belief_auroc"] == pytest.approx(ref["belief_auroc"], abs=2e-3)
+
+
+@pytest.mark.gpu
+def test_c5_belief_auroc_full_size(gpu):
+    """BASELINE C5's belief-head AUROC check at its full env count: 8192 envs of 30x16x99
+    evaluated on device, one episode each. The rule player's belief ranks unknown cells well
+    above chance (the reference run of tests/golden/eval_vec_rule_30x16x99.npz gives 0.788)."""
+    from eval_model import RuleModel
+    from ms_amd import EnvConfig
+    from ms_amd.eval import evaluate_vec
+    got = evaluate_vec(RuleModel().to(gpu), EnvConfig(H=30, W=16, mine_count=99), episodes=8192, seed=1,
+                       num_envs=8192)
+    assert got["episodes"] == 8192
+    assert 0.74 < got["belief_auroc"] < 0.84, got["belief_auroc"]
+    assert 0.0 < got["win_rate"] < 0.1

@@ -1,0 +1,221 @@
+"""Floating-point parity ON THE HIP DEVICE against fixtures captured from the
+reference (north star: "policy logits/values within 1e-5
+fp32"):
+
+* G5 ``model_full_{16x16,9x9,30x16}.npz`` / ``model_small.npz`` /
+  ``model_cnn_9x9.npz``: eval-mode fp32 forward on ``cuda`` within 1e-5
+  (models/cnn_residual.py:83-96, models/cnn.py).
+* G6 ``ppo.npz`` and ``ppo_full_16x16.npz``: one fp32 ``ppo_update`` on ``cuda``
+  (per-tensor path and FlatGrads path) -- stats within 1e-5, the clipped
+  gradients the optimizer stepped on, and the updated parameters
+  (ppo.py:23-119).
+* The production bf16 path (fused MFMA trunk + heads, FlatGrads, bf16
+  autocast) against the same fixtures at a stated bf16 bound: relative L2
+  error <= max(floor, 2 x the error of PyTorch's own bf16 autocast on the same
+  device), the bound the fused-kernel tests use.
+"""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _fp32_highest():
+    prev = torch.get_float32_matmul_precision()
+    torch.set_float32_matmul_precision("highest")
+    yield
+    torch.set_float32_matmul_precision(prev)
+
+
+def _rel(a, b):
+    a, b = torch.as_tensor(a).double().cpu(), torch.as_tensor(b).double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def _full(H, W, dev, dropout=0.05):
+    from ms_amd.models import build_model
+    torch.manual_seed(0)
+    return build_model("cnn_residual", obs_shape=(10, H, W),
+                       model_cfg=dict(stem_channels=96, blocks=5, dropout=dropout, value_hidden=256)).to(dev)
+
+
+def _fwd(m, obs, amp=None):
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp is not None):
+        lg, v, mi = m(obs, return_mine=True)
+    return lg.float().cpu().numpy(), v.float().cpu().numpy(), mi.float().cpu().numpy()
+
+
+@pytest.mark.parametrize("H,W", [(16, 16), (9, 9), (30, 16)])
+def test_full_model_fp32_on_device_matches_reference(gpu, H, W):
+    z = golden(f"model_full_{H}x{W}.npz")
+    m = _full(H, W, gpu).eval()
+    obs = torch.from_numpy(z["obs"]).to(gpu)
+    assert not m.use_fused(obs)  # fp32: the PyTorch-ROCm op chain
+    lg, v, mi = _fwd(m, obs)
+    np.testing.assert_allclose(lg, z["logits"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(v, z["value"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(mi, z["mine"], rtol=0, atol=1e-5)
+
+
+def test_small_and_cnn_models_fp32_on_device(gpu):
+    from ms_amd.models import build_model
+    z = golden("model_small.npz")
+    m = build_model("cnn_residual", obs_shape=(10, 16, 16),
+                    model_cfg=dict(stem_channels=16, blocks=2, dropout=0.05, value_hidden=32))
+    m.load_state_dict({k[3:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("w::")})
+    m = m.to(gpu).eval()
+    lg, v, mi = _fwd(m, torch.from_numpy(z["obs"]).to(gpu))
+    for a, k in ((lg, "logits"), (v, "value"), (mi, "mine")):
+        np.testing.assert_allclose(a, z[k], rtol=0, atol=1e-5, err_msg=k)
+    z = golden("model_cnn_9x9.npz")
+    torch.manual_seed(0)
+    m = build_model("cnn", obs_shape=(10, 9, 9), model_cfg=dict(hidden=64)).to(gpu).eval()
+    lg, v, mi = _fwd(m, torch.from_numpy(z["obs"]).to(gpu))
+    for a, k in ((lg, "logits"), (v, "value"), (mi, "mine")):
+        np.testing.assert_allclose(a, z[k], rtol=0, atol=1e-5, err_msg=k)
+
+
+# bf16 bound for whole-model outputs (fused path and PyTorch bf16 autocast vs fp32 reference)
+BF16_OUT_FLOOR = 2e-2
+
+
+@pytest.mark.parametrize("H,W", [(16, 16), (9, 9), (30, 16)])
+def test_full_model_fused_bf16_matches_reference(gpu, H, W):
+    z = golden(f"model_full_{H}x{W}.npz")
+    m = _full(H, W, gpu).eval()
+    obs = torch.from_numpy(z["obs"]).to(gpu)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        assert m.use_fused(obs)
+    fused = _fwd(m, obs, amp=True)
+    m.fused = False
+    torch_bf16 = _fwd(m, obs, amp=True)
+    for i, k in enumerate(("logits", "value", "mine")):
+        e_f, e_t = _rel(fused[i], z[k]), _rel(torch_bf16[i], z[k])
+        print(f"{H}x{W} {k}: fused {e_f:.3e} torch-bf16 {e_t:.3e}")
+        assert e_f <= max(BF16_OUT_FLOOR, 2 * e_t), (k, e_f, e_t)
+
+
+def _batch(z, dev):
+    from ms_amd.buffers import Batch
+    t = lambda k: torch.from_numpy(z[k]).to(dev)  # noqa: E731
+    return Batch(obs=t("obs"), action_mask=t("mask"), actions=t("actions"), old_logp=t("old_logp"),
+                 values=t("values"), advantages=t("advantages"), returns=t("returns"),
+                 mine_labels=t("mine_labels"), mine_valid=t("mine_valid"))
+
+
+def _record_grads(model, opt):
+    grads = {}
+    step0 = opt.step
+
+    def step(*a, **k):
+        for n, p in model.named_parameters():
+            if p.grad is not None:
+                grads[n] = p.grad.detach().clone()
+        return step0(*a, **k)
+    opt.step = step
+    return grads
+
+
+@pytest.mark.parametrize("flat", [False, True], ids=["per-tensor", "flatgrads"])
+def test_ppo_update_small_fp32_on_device(gpu, flat):
+    from ms_amd.models import build_model
+    from ms_amd.ppo import FlatGrads, PPOConfig, ppo_update
+    z = golden("ppo.npz")
+    m = build_model("cnn_residual", obs_shape=(10, 8, 8),
+                    model_cfg=dict(stem_channels=16, blocks=2, dropout=0.0, value_hidden=32))
+    m.load_state_dict({k[3:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("w::")})
+    m = m.to(gpu)
+    opt = torch.optim.AdamW(m.parameters(), lr=3e-4)
+    cfg = PPOConfig(ent_coef=0.003, aux_mine_weight=0.05, aux_mine_calib_weight=0.01)
+    stats = ppo_update(m, opt, _batch(z, gpu), cfg, scaler=None, amp_dtype=None,
+                       flat_grads=FlatGrads(m.parameters()) if flat else None)
+    ref = dict(zip(z["stat_names"].tolist(), z["stat_values"].tolist()))
+    assert set(stats) == set(ref)
+    for k in ref:
+        assert stats[k] == pytest.approx(ref[k], rel=1e-5, abs=1e-6), k
+    for k, v in m.state_dict().items():
+        np.testing.assert_allclose(v.cpu().numpy(), z["post::" + k], rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+def _full_train(dev):
+    z = golden("ppo_full_16x16.npz")
+    m = _full(16, 16, dev, dropout=0.0)
+    h = hashlib.sha256()
+    for k, v in m.state_dict().items():
+        h.update(k.encode())
+        h.update(v.detach().cpu().contiguous().numpy().tobytes())
+    assert h.hexdigest() == z["init_sha256"].item().decode()  # same initial weights as the reference run
+    return z, m.train()
+
+
+@pytest.mark.parametrize("flat", [False, True], ids=["per-tensor", "flatgrads"])
+def test_ppo_update_full_fp32_on_device(gpu, flat):
+    from ms_amd.ppo import FlatGrads, PPOConfig, ppo_update
+    z, m = _full_train(gpu)
+    opt = torch.optim.AdamW(m.parameters(), lr=3e-4)
+    grads = _record_grads(m, opt)
+    cfg = PPOConfig(ent_coef=0.003, aux_mine_weight=0.05, aux_mine_calib_weight=0.01)
+    stats = ppo_update(m, opt, _batch(z, gpu), cfg, scaler=None, amp_dtype=None,
+                       flat_grads=FlatGrads(m.parameters()) if flat else None)
+    ref = dict(zip(z["stat_names"].tolist(), z["stat_values"].tolist()))
+    assert set(stats) == set(ref)
+    for k in ref:
+        assert stats[k] == pytest.approx(ref[k], rel=1e-5, abs=1e-6), k
+    worst = max(_rel(grads[k], z["grad::" + k]) for k in grads)
+    print(f"full fp32 worst per-tensor grad rel L2 {worst:.3e}")
+    for k in grads:
+        assert _rel(grads[k], z["grad::" + k]) < 1e-4, k
+    for k, v in m.state_dict().items():
+        np.testing.assert_allclose(v.cpu().numpy(), z["post::" + k], rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+def test_ppo_update_full_fused_bf16_trainer_path(gpu):
+    """The Trainer's path: bf16 autocast, fused MFMA trunk + heads, FlatGrads, no scaler.
+    Gradients within max(5e-2, 2 x PyTorch-bf16-autocast error) per tensor of the reference's
+    fp32 gradients; loss terms within 2e-2 relative."""
+    from ms_amd.ppo import FlatGrads, PPOConfig, ppo_update
+    cfg = PPOConfig(ent_coef=0.003, aux_mine_weight=0.05, aux_mine_calib_weight=0.01)
+    res = {}
+    for fused in (True, False):
+        z, m = _full_train(gpu)
+        m.fused = fused
+        opt = torch.optim.AdamW(m.parameters(), lr=3e-4)
+        grads = _record_grads(m, opt)
+        b = _batch(z, gpu)
+        if fused:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                assert m.use_fused(b.obs)
+        stats = ppo_update(m, opt, b, cfg, scaler=None, amp_dtype=torch.bfloat16,
+                           flat_grads=FlatGrads(m.parameters()))
+        res[fused] = (stats, grads, {k: v.detach().cpu() for k, v in m.state_dict().items()})
+    ref = dict(zip(z["stat_names"].tolist(), z["stat_values"].tolist()))
+    stats, grads, post = res[True]
+    for k in ("loss", "policy_loss", "value_loss", "entropy", "aux_bce", "aux_calib"):
+        e = abs(stats[k] - ref[k]) / max(abs(ref[k]), 1e-3)
+        print(f"stat {k}: fused {stats[k]:.6f} ref {ref[k]:.6f} rel {e:.2e} torch-bf16 {res[False][0][k]:.6f}")
+        assert e < 2e-2, k
+    worst = 0.0
+    for k in grads:
+        e_f, e_t = _rel(grads[k], z["grad::" + k]), _rel(res[False][1][k], z["grad::" + k])
+        worst = max(worst, e_f / max(5e-2, 2 * e_t))
+        assert e_f <= max(5e-2, 2 * e_t), (k, e_f, e_t)
+    print(f"worst grad error / bound = {worst:.3f}")
+    # first AdamW step ~ -lr * g/|g|: the update direction must agree with the reference's
+    init = {k: v.detach().cpu() for k, v in _full(16, 16, "cpu", dropout=0.0).state_dict().items()}
+    n_agree = n_tot = 0
+    for k in post:
+        d_ref = torch.from_numpy(z["post::" + k]) - init[k]
+        d_f = post[k] - init[k]
+        big = d_ref.abs() > 1.5e-4  # |update| > lr/2: gradient clearly non-zero
+        n_agree += int((torch.sign(d_f[big]) == torch.sign(d_ref[big])).sum())
+        n_tot += int(big.sum())
+    print(f"update sign agreement {n_agree / n_tot:.4f} over {n_tot} elements")
+    assert n_agree / n_tot > 0.9

@@ -19,7 +19,8 @@ Fixtures
   G5 model_*.npz      CNNResidualPolicy / CNNPolicy eval-mode fp32 outputs
                       (models/cnn_residual.py:30-96, models/cnn.py)
   G6 ppo.npz          one ppo_update on the small model (ppo.py:23-119)
-     ppo_full_16x16.npz one ppo_update on the shipped 96x5 model, with its gradients
+     ppo_full_16x16.npz one ppo_update on the shipped 96x5 model, with its fp32 and
+                      float64 gradients
 """
 from __future__ import annotations
 
@@ -279,47 +280,70 @@ def gen_ppo():
 def gen_ppo_full():
     """G6-full: one ppo_update of the SHIPPED model (96 ch x 5 blocks, seeded init at
     manual_seed(0), dropout 0 so train mode is deterministic) on 64 16x16 samples, fp32,
-    no scaler. Also records the clipped gradients the optimizer stepped on."""
+    no scaler. old_logp / values are the model's own outputs plus small noise (as in a
+    first PPO epoch), so no sample sits at a ratio / value clip boundary and the gradient
+    is a smooth function of the forward pass. Records the clipped gradients the optimizer
+    stepped on (fp32) and the same update run in float64 ("grad64::", the rounding-free
+    truth the fp32 errors are measured against)."""
     torch.set_float32_matmul_precision("highest")
-    torch.manual_seed(0)
     H = W = 16
     A = H * W
-    model = build_model("cnn_residual", obs_shape=(10, H, W),
-                        model_cfg=dict(stem_channels=96, blocks=5, dropout=0.0, value_hidden=256))
-    init = _sd_to_npz(model.state_dict())
-    opt = torch.optim.AdamW(model.parameters(), lr=3e-4)
-    grads = {}
-    step0 = opt.step
-
-    def step_and_record(*a, **k):
-        for n, p in model.named_parameters():
-            grads["grad::" + n] = p.grad.detach().numpy().copy()
-        return step0(*a, **k)
-    opt.step = step_and_record
     B = 64
     g = torch.Generator().manual_seed(13)
     obs = torch.from_numpy(_rand_obs(B, H, W, 14))
     mask = (obs[:, 0] == 0).reshape(B, A)
     mask[:, 0] = True
     actions = torch.multinomial(mask.float(), 1, generator=g).squeeze(1)
-    old_logp = -torch.rand(B, generator=g) * 3 - 4
-    values = torch.randn(B, generator=g) * 0.3
-    adv = torch.randn(B, generator=g)
-    rets = values + adv
     labels = (torch.rand(B, H, W, generator=g) < 0.15).float()
     valid = mask.reshape(B, H, W) & (torch.rand(B, H, W, generator=g) < 0.9)
-    batch = type("Batch", (), dict(obs=obs, action_mask=mask, actions=actions, old_logp=old_logp,
-                                   values=values, advantages=adv, returns=rets,
-                                   mine_labels=labels, mine_valid=valid))
+    n_logp = (torch.rand(B, generator=g) - 0.5) * 0.1
+    n_val = (torch.rand(B, generator=g) - 0.5) * 0.1
+    adv = torch.randn(B, generator=g)
     cfg = PPOConfig(ent_coef=0.003, aux_mine_weight=0.05, aux_mine_calib_weight=0.01)
-    stats = ppo_update(model, opt, batch, cfg, scaler=None)
-    post = {"post::" + k: v.detach().numpy().copy() for k, v in model.state_dict().items()}
+
+    def make(dtype):
+        torch.manual_seed(0)
+        m = build_model("cnn_residual", obs_shape=(10, H, W),
+                        model_cfg=dict(stem_channels=96, blocks=5, dropout=0.0, value_hidden=256))
+        return m.to(dtype)
+
+    model = make(torch.float32)
+    init = _sd_to_npz(model.state_dict())
+    with torch.no_grad():
+        lg, v = model(obs)
+        lp = torch.log_softmax(lg.masked_fill(~mask, -1e9), -1).gather(1, actions[:, None]).squeeze(1)
+    old_logp = (lp + n_logp).float()
+    values = (v.view(-1) + n_val).float()
+    rets = values + adv
+    out = {}
+    for tag, dtype in (("", torch.float32), ("64", torch.float64)):
+        m = model if dtype == torch.float32 else make(dtype)
+        opt = torch.optim.AdamW(m.parameters(), lr=3e-4)
+        grads = {}
+        step0 = opt.step
+
+        def step_and_record(*a, _m=m, _g=grads, _s=step0, **k):
+            for n, p in _m.named_parameters():
+                _g[n] = p.grad.detach().float().numpy().copy()
+            return _s(*a, **k)
+        opt.step = step_and_record
+        c = lambda t: t.to(dtype) if t.is_floating_point() else t  # noqa: E731
+        batch = type("Batch", (), dict(obs=c(obs), action_mask=mask, actions=actions, old_logp=c(old_logp),
+                                       values=c(values), advantages=c(adv), returns=c(rets),
+                                       mine_labels=c(labels), mine_valid=valid))
+        stats = ppo_update(m, opt, batch, cfg, scaler=None)
+        for n, a in grads.items():
+            out[f"grad{tag}::" + n] = a
+        if tag == "":
+            out.update({"post::" + k: v.detach().numpy().copy() for k, v in m.state_dict().items()})
+            out["stat_names"] = np.array(sorted(stats))
+            out["stat_values"] = np.array([stats[k] for k in sorted(stats)])
+        else:
+            out["stat_values64"] = np.array([stats[k] for k in sorted(stats)])
     np.savez_compressed(os.path.join(HERE, "ppo_full_16x16.npz"), obs=obs.numpy(), mask=mask.numpy(),
                         actions=actions.numpy(), old_logp=old_logp.numpy(), values=values.numpy(),
                         advantages=adv.numpy(), returns=rets.numpy(), mine_labels=labels.numpy(),
-                        mine_valid=valid.numpy(), stat_names=np.array(sorted(stats)),
-                        stat_values=np.array([stats[k] for k in sorted(stats)]),
-                        init_sha256=np.bytes_(_sha_sd(init)), **grads, **post)
+                        mine_valid=valid.numpy(), init_sha256=np.bytes_(_sha_sd(init)), **out)
 
 
 def main():

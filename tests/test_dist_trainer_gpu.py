@@ -54,11 +54,12 @@ def _run(rank, world, model, amp, dev):
     cfg, env_d, model_d, extras = _cfg(model)
     info = DistInfo(rank=rank, world=world, local_rank=0, group=dist.group.WORLD if world > 1 else None)
     tr = Trainer(cfg, env_d, model_d, extras, seed=3, info=info, amp=amp, device=dev)
+    init = {k: v.detach().cpu().clone() for k, v in tr.model.state_dict().items()}
     tr.update(0)
     b = tr.buffer
     roll = {k: getattr(b, k).detach().cpu().clone() for k in
             ("obs", "action_mask", "actions", "logp", "rewards", "dones", "values", "mine_labels", "mine_valid")}
-    return roll, {k: v.detach().cpu().clone() for k, v in tr.model.state_dict().items()}, tr.strata
+    return roll, {k: v.detach().cpu().clone() for k, v in tr.model.state_dict().items()}, tr.strata, init
 
 
 def _worker(rank, world, port, out_dir, model, amp):
@@ -69,15 +70,15 @@ def _worker(rank, world, port, out_dir, model, amp):
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
     torch.set_float32_matmul_precision("highest")
-    roll, params, strata = _run(rank, world, model, amp, dev)
+    roll, params, strata, _ = _run(rank, world, model, amp, dev)
     torch.save({"roll": roll, "params": params, "strata": strata}, os.path.join(out_dir, f"r{rank}.pt"))
     dist.destroy_process_group()
 
 
-def _compare(tmp_path, model, amp, atol_noise, tol_fp):
+def _compare(tmp_path, model, amp, atol_noise, tol_fp, tol_delta=None):
     mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), model, amp), nprocs=2, join=True)
     torch.set_float32_matmul_precision("highest")
-    roll1, params1, strata = _run(0, 1, model, amp, torch.device("cuda:0"))
+    roll1, params1, strata, init = _run(0, 1, model, amp, torch.device("cuda:0"))
     r = [torch.load(tmp_path / f"r{i}.pt", weights_only=True) for i in range(2)]
     assert strata == 8 and r[0]["strata"] == r[1]["strata"] == 8
     T, N = 8, 32
@@ -92,11 +93,24 @@ def _compare(tmp_path, model, amp, atol_noise, tol_fp):
     for k, v in params1.items():
         assert torch.equal(r[0]["params"][k], r[1]["params"][k]), k  # ranks stay in lockstep
         d = (r[0]["params"][k] - v).abs()
+        if k == "policy_head.2.bias":
+            # log-softmax is shift invariant: this gradient is 0 in exact arithmetic, so AdamW
+            # turns rounding noise into +-lr steps; only the step-size bound below applies
+            assert float(d.max()) <= 4 * 2 * LR + 1e-6
+            continue
         # AdamW turns summation-order rounding on near-zero gradients into up to +-lr per step
         # (4 steps here); everything else must agree closely
         assert float(d.max()) <= 4 * 2 * LR + 1e-6, k
-        frac_off = float((d > atol_noise).float().mean())
-        assert frac_off < 0.02, (k, frac_off)
+        if tol_delta is None:
+            frac_off = float((d > atol_noise).float().mean())
+            assert frac_off < 0.02, (k, frac_off)
+        else:
+            # bf16: the value head's autocast GEMMs round differently at another batch size, so
+            # compare whole update steps: relative L2 of (2-rank step - 1-rank step)
+            d1, d2 = v - init[k], r[0]["params"][k] - init[k]
+            e = float((d2 - d1).norm() / d1.norm().clamp_min(1e-12))
+            print(f"bf16 DP step error {k}: {e:.3e}")
+            assert e < tol_delta, (k, e)
 
 
 def test_two_rank_trainer_equals_one_rank_fp32(gpu, tmp_path):
@@ -105,4 +119,5 @@ def test_two_rank_trainer_equals_one_rank_fp32(gpu, tmp_path):
 
 def test_two_rank_trainer_equals_one_rank_fused_bf16(gpu, tmp_path):
     """The production path (fused MFMA trunk, bf16 autocast) through the same DP machinery."""
-    _compare(tmp_path, dict(stem_channels=96, blocks=1, value_hidden=32), "bf16", atol_noise=1e-4, tol_fp=1e-2)
+    _compare(tmp_path, dict(stem_channels=96, blocks=1, value_hidden=32), "bf16", atol_noise=None, tol_fp=1e-2,
+             tol_delta=0.1)

@@ -126,23 +126,45 @@ def _record_grads(model, opt):
 
 @pytest.mark.parametrize("flat", [False, True], ids=["per-tensor", "flatgrads"])
 def test_ppo_update_small_fp32_on_device(gpu, flat):
+    """G6 (ppo.npz, small model, random old_logp): stats within 1e-5. Parameters within
+    1e-5/1e-6, except elements whose gradient is too small for its sign to be certain in fp32:
+    AdamW's first step moves every element by ~lr * sign(g), so there the only bound is the
+    step size (the same CPU update, run here, gives the gradients)."""
     from ms_amd.models import build_model
     from ms_amd.ppo import FlatGrads, PPOConfig, ppo_update
     z = golden("ppo.npz")
-    m = build_model("cnn_residual", obs_shape=(10, 8, 8),
-                    model_cfg=dict(stem_channels=16, blocks=2, dropout=0.0, value_hidden=32))
-    m.load_state_dict({k[3:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("w::")})
-    m = m.to(gpu)
-    opt = torch.optim.AdamW(m.parameters(), lr=3e-4)
     cfg = PPOConfig(ent_coef=0.003, aux_mine_weight=0.05, aux_mine_calib_weight=0.01)
-    stats = ppo_update(m, opt, _batch(z, gpu), cfg, scaler=None, amp_dtype=None,
-                       flat_grads=FlatGrads(m.parameters()) if flat else None)
+    runs = {}
+    for dev in ("cpu", gpu):
+        m = build_model("cnn_residual", obs_shape=(10, 8, 8),
+                        model_cfg=dict(stem_channels=16, blocks=2, dropout=0.0, value_hidden=32))
+        m.load_state_dict({k[3:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("w::")})
+        m = m.to(dev)
+        opt = torch.optim.AdamW(m.parameters(), lr=3e-4)
+        grads = _record_grads(m, opt)
+        stats = ppo_update(m, opt, _batch(z, dev), cfg, scaler=None, amp_dtype=None,
+                           flat_grads=FlatGrads(m.parameters()) if (flat and dev != "cpu") else None)
+        runs[str(dev)] = (stats, grads, {k: v.detach().cpu() for k, v in m.state_dict().items()})
+    stats, grads, post = runs[str(gpu)]
+    g_cpu = runs["cpu"][1]
     ref = dict(zip(z["stat_names"].tolist(), z["stat_values"].tolist()))
     assert set(stats) == set(ref)
     for k in ref:
         assert stats[k] == pytest.approx(ref[k], rel=1e-5, abs=1e-6), k
-    for k, v in m.state_dict().items():
-        np.testing.assert_allclose(v.cpu().numpy(), z["post::" + k], rtol=1e-5, atol=1e-6, err_msg=k)
+    _check_adamw_step(post, z, g_cpu, grads)
+
+
+def _check_adamw_step(post, z, g_ref, g_dev, lr=3e-4):
+    for k, v in post.items():
+        want = torch.from_numpy(z["post::" + k])
+        d = (v - want).abs()
+        assert float(d.max()) <= 2 * lr + 1e-6, k
+        if k not in g_ref:
+            continue
+        gr, gd = g_ref[k].cpu(), g_dev[k].cpu()
+        sure = (gr.abs() > 1e-6) & (gr.abs() > 100 * (gd - gr).abs())  # sign certain in fp32
+        bad = sure & (d > 1e-6 + 1e-5 * want.abs())
+        assert not bool(bad.any()), (k, int(bad.sum()), float(d[bad].max()) if bad.any() else 0.0)
 
 
 def _full_train(dev):
@@ -158,6 +180,10 @@ def _full_train(dev):
 
 @pytest.mark.parametrize("flat", [False, True], ids=["per-tensor", "flatgrads"])
 def test_ppo_update_full_fp32_on_device(gpu, flat):
+    """ppo_full_16x16.npz (shipped model, first-epoch-like batch): stats within 1e-5; every
+    gradient tensor within 4x the reference's OWN fp32 error, both measured against the float64
+    run of the same update (the shift-invariant policy_head.2.bias has an exact gradient of 0:
+    bounded relative to the whole gradient instead); the AdamW step as in the small test."""
     from ms_amd.ppo import FlatGrads, PPOConfig, ppo_update
     z, m = _full_train(gpu)
     opt = torch.optim.AdamW(m.parameters(), lr=3e-4)
@@ -169,12 +195,19 @@ def test_ppo_update_full_fp32_on_device(gpu, flat):
     assert set(stats) == set(ref)
     for k in ref:
         assert stats[k] == pytest.approx(ref[k], rel=1e-5, abs=1e-6), k
-    worst = max(_rel(grads[k], z["grad::" + k]) for k in grads)
-    print(f"full fp32 worst per-tensor grad rel L2 {worst:.3e}")
+    gnorm = float(np.sqrt(sum(float((z["grad64::" + k].astype(np.float64) ** 2).sum()) for k in grads)))
+    worst = 0.0
     for k in grads:
-        assert _rel(grads[k], z["grad::" + k]) < 1e-4, k
-    for k, v in m.state_dict().items():
-        np.testing.assert_allclose(v.cpu().numpy(), z["post::" + k], rtol=1e-5, atol=1e-6, err_msg=k)
+        truth = z["grad64::" + k]
+        if k == "policy_head.2.bias":
+            assert float(grads[k].abs().max()) <= 1e-6 * gnorm
+            continue
+        e_dev, e_ref = _rel(grads[k], truth), _rel(z["grad::" + k], truth)
+        worst = max(worst, e_dev / max(e_ref, 1e-6))
+        assert e_dev <= 4 * max(e_ref, 1e-6), (k, e_dev, e_ref)
+    print(f"full fp32: worst gradient error / reference fp32 error = {worst:.2f}")
+    g_ref = {k: torch.from_numpy(z["grad::" + k]) for k in grads}
+    _check_adamw_step({k: v.detach().cpu() for k, v in m.state_dict().items()}, z, g_ref, grads)
 
 
 def test_ppo_update_full_fused_bf16_trainer_path(gpu):
@@ -204,7 +237,9 @@ def test_ppo_update_full_fused_bf16_trainer_path(gpu):
         assert e < 2e-2, k
     worst = 0.0
     for k in grads:
-        e_f, e_t = _rel(grads[k], z["grad::" + k]), _rel(res[False][1][k], z["grad::" + k])
+        if k == "policy_head.2.bias":  # exact gradient 0 (log-softmax shift invariance)
+            continue
+        e_f, e_t = _rel(grads[k], z["grad64::" + k]), _rel(res[False][1][k], z["grad64::" + k])
         worst = max(worst, e_f / max(5e-2, 2 * e_t))
         assert e_f <= max(5e-2, 2 * e_t), (k, e_f, e_t)
     print(f"worst grad error / bound = {worst:.3f}")

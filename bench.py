@@ -62,7 +62,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-multistep", action="store_true", help="skip the one-launch ms_run_tape line")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core in os.sched_getaffinity(0)")
+    ap.add_argument("--extras", default="16x16x40:32768,9x9x10:8192,30x16x99:8192",
+                    help="north-star points (board:envs per GPU) measured after the headline; '' disables")
     ap.add_argument("--diag-no-obs", action="store_true", help="diagnostic: skip obs/mask outputs")
     ap.add_argument("--graph", type=int, default=1, help="capture the timed steps in a HIP graph")
     ap.add_argument("--ppo-updates", type=int, default=2,
@@ -72,38 +74,43 @@ def parse():
     return ap.parse_args()
 
 
+def _cgroup_cpu_quota():
+    """CPUs granted by the cgroup (cpu.max quota / period), or None when unlimited/unknown."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(H, W, K, n_envs, seed, tape, budget_s, threads):
-    """Oracle (CPU restatement, C + pthreads) timed on this host, bounded sample."""
+    """Oracle (CPU restatement of env.py / env_numba, C + pthreads) timed on this host over a
+    bounded sample: each thread owns a block of envs and runs tape action + board step for
+    all of them, step after step, without synchronising (one env per task)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     O.build()
     v = O.OracleVec(H, W, K, n_envs, seed=seed)
     v.reset()
     A = H * W
-    obs = np.zeros((n_envs, 10, H, W), np.float32)
-    mask = np.zeros((n_envs, A), np.uint8)
-    rew = np.zeros(n_envs, np.float32)
-    done = np.zeros(n_envs, np.uint8)
-    st = np.zeros(n_envs, np.int32)
-    ln = np.zeros(n_envs, np.int32)
-    fr = np.zeros(n_envs, np.float64)
-    oc = np.zeros(n_envs, np.int8)
-    act = np.zeros(n_envs, np.int64)
-    for t in range(5):  # warm-up (page in buffers)
-        v.tape(t, tape, out=act)
-        v.step_into(act, obs, mask, rew, done, st, ln, fr, oc, nthreads=threads)
-    steps = 0
+    bufs = (np.zeros((n_envs, 10, H, W), np.float32), np.zeros((n_envs, A), np.uint8),
+            np.zeros(n_envs, np.float32), np.zeros(n_envs, np.uint8), np.zeros(n_envs, np.int32),
+            np.zeros(n_envs, np.int32), np.zeros(n_envs, np.float64), np.zeros(n_envs, np.int8))
+    v.run_baseline(0, 5, tape, threads, bufs)  # warm-up: page in, first clicks
     t0 = time.perf_counter()
-    while True:
-        v.tape(5 + steps, tape, out=act)
-        v.step_into(act, obs, mask, rew, done, st, ln, fr, oc, nthreads=threads)
-        steps += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s and steps >= 3:
-            break
+    v.run_baseline(5, 5, tape, threads, bufs)  # calibrate
+    per_step = (time.perf_counter() - t0) / 5
+    steps = int(max(3, min(200000, budget_s / max(per_step, 1e-9))))
+    t0 = time.perf_counter()
+    v.run_baseline(10, steps, tape, threads, bufs)
+    el = time.perf_counter() - t0
+    quota = _cgroup_cpu_quota()
     return dict(value=n_envs * steps / el, unit="env_steps/s", cores=threads, kind="port",
+                nproc=os.cpu_count(), affinity_cpus=len(os.sched_getaffinity(0)), cgroup_cpu_quota=quota,
                 sample=f"{steps} steps x {n_envs} envs {H}x{W}x{K} (tape {tape}) in {el:.1f}s, "
-                       f"oracle/ms_oracle.c on {threads} pthreads")
+                       f"oracle/ms_oracle.c mso_run_baseline on {threads} threads (one per core in the "
+                       f"affinity mask; nproc {os.cpu_count()}, cgroup quota "
+                       f"{'none' if quota is None else f'{quota:g} CPUs'})")
 
 
 def multistep_bench(args, world, lib, h, L, n_local, n_total, H, W, bpe, dev):
@@ -126,7 +133,8 @@ def multistep_bench(args, world, lib, h, L, n_local, n_total, H, W, bpe, dev):
     ptrs = [L.ptr(b) for b in bufs]
     sp = torch.cuda.current_stream(dev).cuda_stream
     t_base = 1 << 24  # tape indices past those of the per-step measurement
-    L.check(lib.ms_run_tape(h, t_base, min(S, max(1, args.warmup)), args.tape, 1, None, *ptrs, sp))
+    # warm-up: one full S-step launch (so every profiled k_run dispatch but the last is S steps)
+    L.check(lib.ms_run_tape(h, t_base, S, args.tape, 1, None, *ptrs, sp))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -138,7 +146,7 @@ def multistep_bench(args, world, lib, h, L, n_local, n_total, H, W, bpe, dev):
         T = min(S, args.steps - done_steps)
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record()
-        L.check(lib.ms_run_tape(h, t_base + args.warmup + done_steps, T, args.tape, 1, None, *ptrs, sp))
+        L.check(lib.ms_run_tape(h, t_base + S + done_steps, T, args.tape, 1, None, *ptrs, sp))
         ev[1].record()
         evs.append(ev)
         done_steps += T
@@ -211,22 +219,12 @@ def ppo_bench(args, world, rank, local_rank, dev):
             "loss": prof[-1].get("loss"), "entropy": prof[-1].get("entropy")}
 
 
-def main():
-    args = parse()
-    H, W, K = (int(x) for x in args.board.lower().split("x"))
-    args.board_k = K
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
-    torch.cuda.set_device(dev)
-
+def env_bench(args, world, rank, dev, H, W, K, n_local, multistep=True):
+    """Env-step measurement of one board / env count: K graph-replayed (tape + step) steps, the
+    k_step roofline, and (optionally) the multistep ms_run_tape line."""
     from ms_amd import EnvConfig, VecMinesweeper
+    from ms_amd import _lib as L
 
-    n_local = args.envs
     n_total = n_local * world
     vec = VecMinesweeper(n_total, EnvConfig(H=H, W=W, mine_count=K), seed=args.seed, device=dev,
                          shard=(rank, world))
@@ -247,7 +245,6 @@ def main():
     outc = torch.empty(n_local, dtype=torch.int8, device=dev)
     act = torch.empty(n_local, dtype=torch.int64, device=dev)
     lib, h = vec._lib, vec._h
-    from ms_amd import _lib as L
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
     ptrs = [L.ptr(x) for x in (act, obs, mask, rew, done, step_i, lnew, frac, outc)]
@@ -317,6 +314,7 @@ def main():
         span_tape = ev_tape[0].elapsed_time(ev_tape[1])
         kern_ms = (span_full - span_tape) / args.steps
         kern_method = "graph span difference (tape+step vs tape only) / K"
+        del gt
     else:
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                for _ in range(args.steps)]
@@ -331,19 +329,48 @@ def main():
         elapsed, kern_ms = float(t[0]), float(t[1])
 
     traffic, traffic_src = pmc_traffic(H, W, K, n_local)
-    total_env_steps = n_total * args.steps
-    value = total_env_steps / elapsed
     bpe = algo_bytes_per_env_step(H, W)
     achieved = bpe * n_local / (kern_ms * 1e-3) / 1e9
+    res = {"board": f"{H}x{W}x{K}", "envs_per_gpu": n_local, "envs_total": n_total,
+           "value": n_total * args.steps / elapsed, "unit": "env_steps/s",
+           "ms_per_step": elapsed / args.steps * 1e3, "obs_ring_slots": R,
+           "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                        "kernel": "k_step", "kernel_ms": kern_ms, "kernel_ms_method": kern_method,
+                        "algo_bytes_per_env_step": bpe,
+                        "algo_bytes_per_launch": bpe * n_local, "traffic_source": traffic_src}}
+    del graph
+    if multistep and not args.diag_no_obs:
+        args.board_k = K
+        res["multistep"] = multistep_bench(args, world, lib, h, L, n_local, n_total, H, W, bpe, dev)
+    del vec, obs_ring, mask_ring
+    torch.cuda.empty_cache()
+    return res
 
+
+def main():
+    args = parse()
+    H, W, K = (int(x) for x in args.board.lower().split("x"))
+    args.board_k = K
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    n_local = args.envs
+    head = env_bench(args, world, rank, dev, H, W, K, n_local, multistep=not args.no_multistep)
     out = {
         "metric": "env steps/sec (16x16x40, N envs) + PPO updates/sec at 1/2/4/8 MI355X",
-        "value": value,
+        "value": head["value"],
         "unit": "env_steps/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": head["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -351,24 +378,29 @@ def main():
         "data": "synthetic: numpy-seeded boards, splitmix64 action tape (SURVEY.md §8d)",
         "config": {"workload": f"board step {H}x{W}x{K}, {n_local} envs per GPU (BASELINE configs[1]"
                                f"{', configs[3] at 8 GPUs' if world == 8 else ''})",
-                   "board": f"{H}x{W}x{K}", "envs_per_gpu": n_local, "envs_total": n_total,
+                   "board": f"{H}x{W}x{K}", "envs_per_gpu": n_local, "envs_total": n_local * world,
                    "tape": args.tape, "parallelism": f"env-shard x{world}, no collective",
-                   "obs_ring_slots": R},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_step", "kernel_ms": kern_ms, "kernel_ms_method": kern_method,
-                     "algo_bytes_per_env_step": bpe,
-                     "algo_bytes_per_launch": bpe * n_local, "traffic_source": traffic_src},
+                   "obs_ring_slots": head["obs_ring_slots"]},
+        "roofline": head["roofline"],
     }
-    if not args.no_multistep and not args.diag_no_obs:
-        out["multistep"] = multistep_bench(args, world, lib, h, L, n_local, n_total, H, W, bpe, dev)
+    if "multistep" in head:
+        out["multistep"] = head["multistep"]
+    if args.extras and not args.diag_no_obs:
+        pts = []
+        for item in args.extras.split(","):
+            b, n = item.split(":")
+            h_, w_, k_ = (int(x) for x in b.lower().split("x"))
+            r = env_bench(args, world, rank, dev, h_, w_, k_, int(n), multistep=not args.no_multistep)
+            pts.append(r)
+        out["north_star_points"] = pts
     if args.ppo_updates > 0:
         out["ppo"] = ppo_bench(args, world, rank, local_rank, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        threads = args.cpu_threads or len(os.sched_getaffinity(0))
         out["cpu_baseline"] = cpu_baseline(H, W, K, n_local, args.seed, args.tape, args.cpu_seconds,
                                            threads)
-        out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+        out["gpu_over_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+        out["gpu_over_cpu_target"] = 50.0
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -708,36 +708,112 @@ static inline uint64_t splitmix64(uint64_t x) {
 
 uint64_t mso_splitmix64(uint64_t x) { return splitmix64(x); }
 
-int mso_tape_actions(mso_vec* v, uint64_t t, int32_t mode, int64_t* actions) {
+/* SURVEY.md §8d action tape for env i at step t (same rule as ms_tape_actions) */
+static int64_t tape_one(const mso_vec* v, int64_t i, uint64_t t, int32_t mode) {
   const int A = v->A;
+  const env_t* e = &v->envs[i];
+  uint64_t g = (uint64_t)(v->env_begin + i);
+  uint64_t x = splitmix64(0xC0FFEEULL ^ (g << 32) ^ t);
+  int n_valid = 0, n_safe = 0;
+  for (int k = 0; k < A; k++) {
+    n_valid += !e->revealed[k];
+    n_safe += (!e->revealed[k] && !e->mine[k]);
+  }
+  int want_safe = (mode == MS_TAPE_SAFE_BIASED) && ((x & 0xFFFFu) < 65208u) && n_safe > 0;
+  int64_t act = 0;
+  if (want_safe) {
+    int target = (int)((x >> 16) % (uint64_t)n_safe);
+    for (int k = 0; k < A; k++)
+      if (!e->revealed[k] && !e->mine[k] && target-- == 0) {
+        act = k;
+        break;
+      }
+  } else if (n_valid > 0) {
+    uint64_t sel = (mode == MS_TAPE_SAFE_BIASED) ? (x >> 16) : x;
+    int target = (int)(sel % (uint64_t)n_valid);
+    for (int k = 0; k < A; k++)
+      if (!e->revealed[k] && target-- == 0) {
+        act = k;
+        break;
+      }
+  }
+  return act;
+}
+
+/* CPU baseline (bench.py cpu_baseline): `steps` consecutive (tape action, board step) pairs
+ * for every env, on a pool of nthreads threads that each own a contiguous block of envs for
+ * the whole run. Envs are independent (no shared RNG without late start), so the threads
+ * never synchronise: the per-env sequential algorithm of env_numba / env.py, one env per
+ * task, over every core given. Outputs go to caller buffers sized for all envs (each env's
+ * slot is overwritten every step). */
+typedef struct {
+  step_job_t j;
+  uint64_t t0;
+  int64_t steps;
+  int32_t mode;
+} run_job_t;
+
+static void* run_thread(void* p) {
+  run_job_t* r = (run_job_t*)p;
+  step_job_t* j = &r->j;
+  int64_t* act = (int64_t*)malloc(sizeof(int64_t) * (size_t)(j->e > j->b ? j->e : 1));
+  if (!act) return NULL;
+  int64_t* a_full = act - j->b;  /* index by global env id within this handle */
+  j->a64 = a_full;
+  for (int64_t s = 0; s < r->steps; s++) {
+    for (int64_t i = j->b; i < j->e; i++) a_full[i] = tape_one(j->v, i, r->t0 + (uint64_t)s, r->mode);
+    step_range(j);
+  }
+  free(act);
+  return NULL;
+}
+
+int mso_run_baseline(mso_vec* v, uint64_t t0, int64_t steps, int32_t mode, int32_t nthreads, float* obs,
+                     uint8_t* mask, float* reward, uint8_t* done, int32_t* step, int32_t* last_new,
+                     double* frac, int8_t* outcome) {
+  if (!v || steps < 0) {
+    snprintf(g_err, sizeof g_err, "mso_run_baseline: bad argument");
+    return MS_EINVAL;
+  }
+  if (nthreads < 1 || v->late_on) nthreads = 1;
+  if (nthreads > v->n) nthreads = (int)v->n;
+  if (nthreads > 1024) nthreads = 1024;
+  run_job_t* jobs = (run_job_t*)calloc((size_t)nthreads, sizeof(run_job_t));
+  pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+  if (!jobs || !th) {
+    free(jobs);
+    free(th);
+    snprintf(g_err, sizeof g_err, "mso_run_baseline: out of memory");
+    return MS_EINVAL;
+  }
+  for (int t = 0; t < nthreads; t++) {
+    step_job_t* j = &jobs[t].j;
+    j->v = v;
+    j->b = v->n * t / nthreads;
+    j->e = v->n * (t + 1) / nthreads;
+    j->obs = obs;
+    j->mask = mask;
+    j->reward = reward;
+    j->done = done;
+    j->step = step;
+    j->last_new = last_new;
+    j->frac = frac;
+    j->outcome = outcome;
+    jobs[t].t0 = t0;
+    jobs[t].steps = steps;
+    jobs[t].mode = mode;
+  }
+  for (int t = 1; t < nthreads; t++) pthread_create(&th[t], NULL, run_thread, &jobs[t]);
+  run_thread(&jobs[0]);
+  for (int t = 1; t < nthreads; t++) pthread_join(th[t], NULL);
+  free(jobs);
+  free(th);
+  return MS_OK;
+}
+
+int mso_tape_actions(mso_vec* v, uint64_t t, int32_t mode, int64_t* actions) {
   for (int64_t i = 0; i < v->n; i++) {
-    const env_t* e = &v->envs[i];
-    uint64_t g = (uint64_t)(v->env_begin + i);
-    uint64_t x = splitmix64(0xC0FFEEULL ^ (g << 32) ^ t);
-    int n_valid = 0, n_safe = 0;
-    for (int k = 0; k < A; k++) {
-      n_valid += !e->revealed[k];
-      n_safe += (!e->revealed[k] && !e->mine[k]);
-    }
-    int want_safe = (mode == MS_TAPE_SAFE_BIASED) && ((x & 0xFFFFu) < 65208u) && n_safe > 0;
-    int64_t act = 0;
-    if (want_safe) {
-      int target = (int)((x >> 16) % (uint64_t)n_safe);
-      for (int k = 0; k < A; k++)
-        if (!e->revealed[k] && !e->mine[k] && target-- == 0) {
-          act = k;
-          break;
-        }
-    } else if (n_valid > 0) {
-      uint64_t sel = (mode == MS_TAPE_SAFE_BIASED) ? (x >> 16) : x;
-      int target = (int)(sel % (uint64_t)n_valid);
-      for (int k = 0; k < A; k++)
-        if (!e->revealed[k] && target-- == 0) {
-          act = k;
-          break;
-        }
-    }
-    actions[i] = act;
+    actions[i] = tape_one(v, i, t, mode);
   }
   return MS_OK;
 }

@@ -52,6 +52,7 @@ def lib():
         L.mso_snapshot.argtypes = [vp, vp, vp, vp, vp, vp]
         L.mso_rng_state.argtypes = [vp, vp]
         L.mso_tape_actions.argtypes = [vp, u64, i32, vp]
+        L.mso_run_baseline.argtypes = [vp, u64, i64, i32, i32] + [vp] * 8
         L.mso_gae.argtypes = [vp, vp, vp, vp, i32, i64, ctypes.c_float, ctypes.c_float, vp, vp]
         L.mso_gae.restype = None
         L.mso_seed_state.argtypes = [u64, vp]
@@ -154,6 +155,12 @@ class OracleVec:
         out = np.zeros((self.n, 6), np.uint64)
         _check(lib().mso_rng_state(self._h, _p(out)))
         return out
+
+    def run_baseline(self, t0, steps, mode, nthreads, bufs):
+        """CPU baseline: ``steps`` x (tape action + board step) for every env on ``nthreads``
+        threads that each own a block of envs for the whole run (no per-step sync).
+        ``bufs`` = (obs, mask, rew, done, step, lnew, frac, outc) caller arrays."""
+        _check(lib().mso_run_baseline(self._h, t0, steps, mode, nthreads, *[_p(b) for b in bufs]))
 
     def tape(self, t, mode=0, out=None):
         a = np.zeros(self.n, np.int64) if out is None else out

@@ -149,3 +149,23 @@ def test_negative_and_large_actions_wrap_python_style():
     for k in ("reward", "done", "step", "last_new", "frac"):
         assert np.array_equal(o1[k], o2[k])
     assert np.array_equal(o1["obs"], o2["obs"])
+
+
+def test_cpu_baseline_runner_equals_step_loop():
+    """mso_run_baseline (bench.py's cpu_baseline: per-thread env blocks, no per-step sync) is
+    the same computation as T x (tape + step) over the batch."""
+    import oracle as O
+    H, W, K, N, T = 9, 9, 10, 96, 25
+    a, b = O.OracleVec(H, W, K, N, seed=4), O.OracleVec(H, W, K, N, seed=4)
+    a.reset()
+    b.reset()
+    for t in range(T):
+        a.step(a.tape(t, 1))
+    bufs = (np.zeros((N, 10, H, W), np.float32), np.zeros((N, H * W), np.uint8), np.zeros(N, np.float32),
+            np.zeros(N, np.uint8), np.zeros(N, np.int32), np.zeros(N, np.int32), np.zeros(N, np.float64),
+            np.zeros(N, np.int8))
+    b.run_baseline(0, T, 1, 5, bufs)
+    assert np.array_equal(a.rng_state(), b.rng_state())
+    sa, sb = a.snapshot(), b.snapshot()
+    for k in sa:
+        assert np.array_equal(sa[k], sb[k]), k

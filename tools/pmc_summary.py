@@ -38,7 +38,17 @@ ap.add_argument("--config", default="16x16x40, 4096 envs, tape 0")
 ap.add_argument("--algo-bytes", type=int, default=4096 * 10729)
 ap.add_argument("--command", default="")
 ap.add_argument("--steps-per-launch", type=int, default=1, help="env steps one launch performs (k_run: S)")
+ap.add_argument("--bench-log", default=None,
+                help="log of the profiled bench.py run: its JSON line gives k_run's steps per launch")
+ap.add_argument("--fetch-wide", action="store_true",
+                help="double FETCH_SIZE (gfx950 reports half of 16-B/lane streaming reads)")
 a = ap.parse_args()
+if a.bench_log:
+    line = [x for x in open(a.bench_log).read().splitlines() if x.startswith("{")][-1]
+    ms = json.loads(line).get("multistep")
+    if a.kernel == "k_run" and ms:
+        a.steps_per_launch = int(ms["roofline"]["steps_per_launch"])
+        a.algo_bytes = a.algo_bytes * a.steps_per_launch
 fe, wr = load(a.fetch, "FETCH_SIZE"), load(a.write, "WRITE_SIZE")
 allk = {}
 for k in sorted(set(fe) | set(wr)):
@@ -46,14 +56,15 @@ for k in sorted(set(fe) | set(wr)):
     allk[k] = {"FETCH_SIZE_KB_mean": sum(fv) / max(1, len(fv)), "WRITE_SIZE_KB_mean": sum(wv) / max(1, len(wv)),
                "dispatches": max(len(fv), len(wv))}
 name = next(k for k in allk if a.kernel in k)
-fb = allk[name]["FETCH_SIZE_KB_mean"] * 1024
+fb = allk[name]["FETCH_SIZE_KB_mean"] * 1024 * (2 if a.fetch_wide else 1)
 wb = allk[name]["WRITE_SIZE_KB_mean"] * 1024
 out = {"command": a.command, "kernel": name, "config": a.config, "fetch_bytes_per_launch": fb,
        "write_bytes_per_launch": wb, "traffic_bytes_per_launch": fb + wb,
        "algorithmic_bytes_per_launch": a.algo_bytes, "steps_per_launch": a.steps_per_launch,
        "traffic_bytes_per_step": (fb + wb) / a.steps_per_launch,
-       "note": "FETCH_SIZE taken as reported (small scattered state loads, not 16-B/lane streams); "
-               "WRITE_SIZE exact for the dwordx4 obs stores",
+       "note": ("FETCH_SIZE doubled (16-B/lane streaming reads, MI355X_MICROARCH.md HBM note)" if a.fetch_wide else
+                "FETCH_SIZE taken as reported (small scattered state loads, not 16-B/lane streams)")
+               + "; WRITE_SIZE exact for 16-B/lane stores",
        "all_kernels": allk}
 json.dump(out, open(a.out, "w"), indent=1)
 print(json.dumps({k: out[k] for k in ("kernel", "traffic_bytes_per_launch", "algorithmic_bytes_per_launch")}))

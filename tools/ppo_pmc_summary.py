@@ -1,0 +1,68 @@
+"""Per-kernel summary of the PPO minibatch passes (tools/profile_round.sh step 3): trace
+duration, HBM traffic (FETCH_SIZE doubled for the trunk kernels' 16-B/lane streaming reads,
+MI355X_MICROARCH.md HBM note; WRITE_SIZE as reported), MFMA busy fraction
+(SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)) and, for the 96->96
+trunk layers, achieved TFLOP/s on the algorithmic 2*N*P*96*96*9 flops of one launch."""
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--fetch", required=True)
+ap.add_argument("--write", required=True)
+ap.add_argument("--mfma", required=True)
+ap.add_argument("--trace", required=True)
+ap.add_argument("--samples", type=int, default=32768)
+ap.add_argument("--pixels", type=int, default=256)
+ap.add_argument("--out", required=True)
+a = ap.parse_args()
+
+
+def counters(d, name):
+    per = defaultdict(list)
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        acc = defaultdict(float)
+        kern = {}
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") != name:
+                continue
+            key = r.get("Dispatch_Id", r.get("Correlation_Id"))
+            acc[key] += float(r["Counter_Value"])
+            kern[key] = r["Kernel_Name"]
+        for k, v in acc.items():
+            per[kern[k]].append(v)
+    return {k: sum(v) / len(v) for k, v in per.items()}
+
+
+dur = defaultdict(list)
+for f in glob.glob(os.path.join(a.trace, "**", "*kernel_trace.csv"), recursive=True):
+    for r in csv.DictReader(open(f)):
+        dur[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+fe, wr = counters(a.fetch, "FETCH_SIZE"), counters(a.write, "WRITE_SIZE")
+mb, gui = counters(a.mfma, "SQ_VALU_MFMA_BUSY_CYCLES"), counters(a.mfma, "GRBM_GUI_ACTIVE")
+flops96 = 2.0 * a.samples * a.pixels * 96 * 96 * 9
+rows = {}
+for k, ds in dur.items():
+    if not any(t in k for t in ("k_conv_gn_fwd", "k_bwd_data", "k_wgrad", "k_heads", "k_reduce")):
+        continue
+    us = sum(ds) / len(ds)
+    wide = any(t in k for t in ("k_conv_gn_fwd", "k_bwd_data", "k_wgrad", "k_heads"))
+    fb = fe.get(k, 0.0) * 1024 * (2 if wide else 1)
+    wb = wr.get(k, 0.0) * 1024
+    rec = {"launches": len(ds), "mean_us": us, "fetch_bytes": fb, "write_bytes": wb,
+           "traffic_bytes": fb + wb, "hbm_GBps": (fb + wb) / (us * 1e-6) / 1e9 if us > 0 else None,
+           "fetch_doubled": wide}
+    if k in mb and gui.get(k):
+        rec["mfma_busy_frac"] = mb[k] / (gui[k] / 8.0 * 1024.0)
+    if ("<96" in k or "96," in k) and any(t in k for t in ("k_conv_gn_fwd", "k_bwd_data", "k_wgrad")):
+        rec["algo_tflop"] = flops96 / 1e12
+        rec["achieved_TFLOPs"] = flops96 / (us * 1e-6) / 1e12
+        rec["mfma_frac_of_2500"] = rec["achieved_TFLOPs"] / 2500.0
+    rows[k] = rec
+json.dump({"samples": a.samples, "kernels": rows}, open(a.out, "w"), indent=1)
+for k, r in sorted(rows.items(), key=lambda kv: -kv[1]["mean_us"] * kv[1]["launches"]):
+    print(f"{r['mean_us']:9.1f} us x{r['launches']:3d} traffic {r['traffic_bytes'] / 1e9:6.2f} GB "
+          f"mfma_busy {r.get('mfma_busy_frac', float('nan')):.3f} {k[:90]}")

@@ -113,6 +113,41 @@ def cpu_baseline(H, W, K, n_envs, seed, tape, budget_s, threads):
                        f"{'none' if quota is None else f'{quota:g} CPUs'})")
 
 
+class DispatchTimer:
+    """Pairs of HIP events stamped by the kernel dispatch itself (ms_set_timing_events ->
+    hipExtLaunchKernel): elapsed = the kernel's execution time as rocprofv3 traces it."""
+
+    def __init__(self, lib, L, h, n):
+        import ctypes
+        self.lib, self.L, self.h = lib, L, h
+        self.ev = []
+        for _ in range(n):
+            pair = []
+            for _ in range(2):
+                e = ctypes.c_void_p()
+                L.check(lib.ms_event_create(ctypes.byref(e)))
+                pair.append(e.value)
+            self.ev.append(pair)
+
+    def arm(self, i):
+        self.L.check(self.lib.ms_set_timing_events(self.h, self.ev[i][0], self.ev[i][1]))
+
+    def disarm(self):
+        self.L.check(self.lib.ms_set_timing_events(self.h, None, None))
+
+    def elapsed_ms(self, i):
+        import ctypes
+        ms = ctypes.c_float()
+        self.L.check(self.lib.ms_event_elapsed_ms(self.ev[i][0], self.ev[i][1], ctypes.byref(ms)))
+        return ms.value
+
+    def close(self):
+        self.disarm()
+        for pair in self.ev:
+            for e in pair:
+                self.lib.ms_event_destroy(e)
+
+
 def multistep_bench(args, world, lib, h, L, n_local, n_total, H, W, bpe, dev):
     """ms_run_tape: the same synthetic tape + board step, S steps per launch (boards held
     in registers between steps), every step's outputs in their own slot as in a rollout
@@ -139,22 +174,23 @@ def multistep_bench(args, world, lib, h, L, n_local, n_total, H, W, bpe, dev):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    evs = []
+    n_launch = -(-args.steps // S)
+    timer = DispatchTimer(lib, L, h, n_launch)
     t0 = time.perf_counter()
     done_steps = 0
+    i = 0
     while done_steps < args.steps:
         T = min(S, args.steps - done_steps)
-        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-        ev[0].record()
+        timer.arm(i)
         L.check(lib.ms_run_tape(h, t_base + S + done_steps, T, args.tape, 1, None, *ptrs, sp))
-        ev[1].record()
-        evs.append(ev)
         done_steps += T
+        i += 1
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    kern_ms = sum(timer.elapsed_ms(j) for j in range(n_launch)) / args.steps
+    timer.close()
     if world > 1:
         t = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -167,7 +203,8 @@ def multistep_bench(args, world, lib, h, L, n_local, n_total, H, W, bpe, dev):
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes per step",
                          "traffic_source": traffic_src, "kernel": "k_run",
                          "kernel_ms_per_step": kern_ms, "steps_per_launch": S,
-                         "kernel_ms_method": "HIP events around each S-step launch, summed / K"}}
+                         "kernel_ms_method": "dispatch-stamped HIP events (hipExtLaunchKernel) of each "
+                                             "S-step launch, summed / K"}}
 
 
 # fwd / fwd+bwd GFLOP per 16x16 sample of the shipped model (torch flop counter)
@@ -282,47 +319,41 @@ def env_bench(args, world, rank, dev, H, W, K, n_local, multistep=True):
         return g  # capture does not execute: the board state is still at step `warmup`
 
     graph = capture(False) if args.graph else None
-    ev_full = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    ev_full[0].record()
     if graph is not None:
         graph.replay()
     else:
         for k in range(args.steps):
             one_step(args.warmup + k, sp)
-    ev_full[1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
-    # Dominant-kernel duration from HIP events on the launch stream: the span of
-    # the K-step graph minus the span of a graph holding only its K tape
-    # launches, divided by K = what one ms_step adds to a step, boundary
-    # included (rocprofv3's per-dispatch average is in profiles/).
-    if graph is not None:
-        gt = capture(True)
-        ev_tape = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-        ev_tape[0].record()
-        gt.replay()
-        ev_tape[1].record()
-        torch.cuda.synchronize()
-        span_full = ev_full[0].elapsed_time(ev_full[1])
-        span_tape = ev_tape[0].elapsed_time(ev_tape[1])
-        kern_ms = (span_full - span_tape) / args.steps
-        kern_method = "graph span difference (tape+step vs tape only) / K"
-        del gt
-    else:
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(args.steps)]
-        for k in range(args.steps):
-            one_step(args.warmup + args.steps + k, sp, evs[k])
-        torch.cuda.synchronize()
-        kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-        kern_method = "events around each ms_step (eager)"
+    # Dominant-kernel duration: after the timed region, K more eager steps whose k_step
+    # dispatches stamp their own HIP events (hipExtLaunchKernel via ms_set_timing_events),
+    # i.e. each launch's execution time as rocprofv3's kernel trace reports it (the per-step
+    # time above additionally holds k_tape and the launch boundaries).
+    del graph
+    graph = None
+    n_t = args.steps
+    timer = DispatchTimer(lib, L, h, n_t)
+    for k in range(n_t):
+        L.check(lib.ms_tape_actions(h, args.warmup + args.steps + k, args.tape, ptrs[0], sp))
+        pt = list(ptrs)
+        if not args.diag_no_obs:
+            t_ = args.warmup + args.steps + k
+            pt[1], pt[2] = L.ptr(obs_ring[t_ % R]), L.ptr(mask_ring[t_ % R])
+        timer.arm(k)
+        L.check(lib.ms_step(h, *pt, sp))
+    timer.disarm()
+    torch.cuda.synchronize()
+    kern_ms = float(np.mean([timer.elapsed_ms(k) for k in range(n_t)]))
+    timer.close()
+    kern_method = "mean of dispatch-stamped HIP events (hipExtLaunchKernel) over K eager k_step launches"
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -339,7 +370,6 @@ def env_bench(args, world, rank, dev, H, W, K, n_local, multistep=True):
                         "kernel": "k_step", "kernel_ms": kern_ms, "kernel_ms_method": kern_method,
                         "algo_bytes_per_env_step": bpe,
                         "algo_bytes_per_launch": bpe * n_local, "traffic_source": traffic_src}}
-    del graph
     if multistep and not args.diag_no_obs:
         args.board_k = K
         res["multistep"] = multistep_bench(args, world, lib, h, L, n_local, n_total, H, W, bpe, dev)

@@ -19,6 +19,16 @@ extern "C" {
 
 int ms_set_debug_flags(ms_handle* h, uint32_t flags);
 
+/* Measurement (bench.py): while set, every k_step / k_run launch of this handle is
+ * dispatched with hipExtLaunchKernel(start_event, stop_event), so the events are stamped
+ * by the dispatch itself and bracket exactly the kernel's execution (what rocprofv3's
+ * kernel trace reports), without the launch gap a stream event would include.
+ * NULL, NULL restores plain launches. Not for graph capture. */
+int ms_set_timing_events(ms_handle* h, void* start_event, void* stop_event);
+int ms_event_create(void** event);
+int ms_event_elapsed_ms(void* start_event, void* stop_event, float* ms);
+int ms_event_destroy(void* event);
+
 /* libmsenv_diag.so only: per-env s_memtime/s_memrealtime stamps, device
  * u64[env_count][8] (NULL disables). Ignored by the production build. */
 int ms_set_diag(ms_handle* h, uint64_t* stamps);

@@ -22,6 +22,7 @@
 // observation, which is ~97% of the bytes a step moves, is emitted as
 // coalesced 16-B stores (one 1 KiB wave-instruction per channel plane on
 // 16x16) from a per-cell code computed from LDS-staged rows.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -1486,6 +1487,7 @@ struct ms_handle {
   uint32_t dbg_flags;
   int epw;         // boards per workgroup of k_step (MSENV_EPW overrides, tools only)
   int late_on;     // ms_set_late_start called with prob > 0
+  hipEvent_t ev_start, ev_stop;  // ms_set_timing_events (measurement only): stamp k_step / k_run
   LateCfg late;
   Pcg* late_rng;   // device: the shared late-start generator
 };
@@ -1497,20 +1499,23 @@ bool shape_ok(const ms_cfg* c) {
          c->mine_count < c->H * c->W;
 }
 
+// ev0/ev1 non-null (ms_set_timing_events): the dispatch itself stamps the events, so their
+// difference is the kernel's execution time as the profiler sees it (no launch gap)
 template <int H_, int W_>
-void launch_step(const KParams& p, int epw, hipStream_t s) {
+void launch_step(const KParams& p, int epw, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   // generic shapes keep one board per workgroup (their LDS table is sized for 64x62)
   if (H_ && W_ && epw == 4) {
-    hipLaunchKernelGGL((k_step<H_, W_, 4>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, p);
+    hipExtLaunchKernelGGL((k_step<H_, W_, 4>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, ev0, ev1, 0, p);
   } else {
-    hipLaunchKernelGGL((k_step<H_, W_, 1>), dim3((unsigned)p.n), dim3(64), 0, s, p);
+    hipExtLaunchKernelGGL((k_step<H_, W_, 1>), dim3((unsigned)p.n), dim3(64), 0, s, ev0, ev1, 0, p);
   }
 }
 
 template <int H_, int W_>
-void launch_run(const KParams& p, const RunParams& r, hipStream_t s) {
-  if (H_ && W_) hipLaunchKernelGGL((k_run<H_, W_, 4>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, p, r);
-  else hipLaunchKernelGGL((k_run<H_, W_, 1>), dim3((unsigned)p.n), dim3(64), 0, s, p, r);
+void launch_run(const KParams& p, const RunParams& r, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+  if (H_ && W_)
+    hipExtLaunchKernelGGL((k_run<H_, W_, 4>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, ev0, ev1, 0, p, r);
+  else hipExtLaunchKernelGGL((k_run<H_, W_, 1>), dim3((unsigned)p.n), dim3(64), 0, s, ev0, ev1, 0, p, r);
 }
 
 template <int H_, int W_>
@@ -1561,12 +1566,12 @@ int do_step(ms_handle* h, const void* actions, int i32, float* obs, uint8_t* mas
   p.actions_i32 = i32;
   hipStream_t s = (hipStream_t)stream;
   if (h->late_on && !done) return fail(MS_EINVAL, "ms_step: late start needs the done output");
-  if (h->H == 16 && h->W == 16) launch_step<16, 16>(p, h->epw, s);
-  else if (h->H == 9 && h->W == 9) launch_step<9, 9>(p, h->epw, s);
-  else if (h->H == 30 && h->W == 16) launch_step<30, 16>(p, h->epw, s);
-  else if (h->H == 16 && h->W == 30) launch_step<16, 30>(p, h->epw, s);
-  else if (h->H == 8 && h->W == 8) launch_step<8, 8>(p, h->epw, s);
-  else launch_step<0, 0>(p, h->epw, s);
+  if (h->H == 16 && h->W == 16) launch_step<16, 16>(p, h->epw, s, h->ev_start, h->ev_stop);
+  else if (h->H == 9 && h->W == 9) launch_step<9, 9>(p, h->epw, s, h->ev_start, h->ev_stop);
+  else if (h->H == 30 && h->W == 16) launch_step<30, 16>(p, h->epw, s, h->ev_start, h->ev_stop);
+  else if (h->H == 16 && h->W == 30) launch_step<16, 30>(p, h->epw, s, h->ev_start, h->ev_stop);
+  else if (h->H == 8 && h->W == 8) launch_step<8, 8>(p, h->epw, s, h->ev_start, h->ev_stop);
+  else launch_step<0, 0>(p, h->epw, s, h->ev_start, h->ev_stop);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "ms_step launch");
   // auto-resets that draw a late start (env.py:497-498 -> 406-414), in env order
@@ -1680,6 +1685,33 @@ int ms_set_debug_flags(ms_handle* h, uint32_t flags) {
   return MS_OK;
 }
 
+int ms_set_timing_events(ms_handle* h, void* start_event, void* stop_event) {
+  if (!h) return fail(MS_EINVAL, "ms_set_timing_events: null handle");
+  h->ev_start = (hipEvent_t)start_event;
+  h->ev_stop = (hipEvent_t)stop_event;
+  return MS_OK;
+}
+
+int ms_event_create(void** event) {
+  if (!event) return fail(MS_EINVAL, "ms_event_create: null argument");
+  hipEvent_t e = nullptr;
+  hipError_t r = hipEventCreate(&e);
+  if (r != hipSuccess) return hip_fail(r, "hipEventCreate");
+  *event = (void*)e;
+  return MS_OK;
+}
+
+int ms_event_elapsed_ms(void* start_event, void* stop_event, float* ms) {
+  if (!start_event || !stop_event || !ms) return fail(MS_EINVAL, "ms_event_elapsed_ms: null argument");
+  hipError_t r = hipEventElapsedTime(ms, (hipEvent_t)start_event, (hipEvent_t)stop_event);
+  return r == hipSuccess ? MS_OK : hip_fail(r, "hipEventElapsedTime");
+}
+
+int ms_event_destroy(void* event) {
+  if (event) hipEventDestroy((hipEvent_t)event);
+  return MS_OK;
+}
+
 int ms_set_diag(ms_handle* h, uint64_t* stamps) {
   if (!h) return fail(MS_EINVAL, "ms_set_diag: null handle");
   h->diag = stamps;
@@ -1786,12 +1818,12 @@ int ms_run_tape(ms_handle* h, uint64_t t0, int32_t T, int32_t mode, int32_t slot
   r.env_begin = h->env_begin;
   r.actions = actions;
   const hipStream_t s = (hipStream_t)stream;
-  if (h->H == 16 && h->W == 16) launch_run<16, 16>(p, r, s);
-  else if (h->H == 9 && h->W == 9) launch_run<9, 9>(p, r, s);
-  else if (h->H == 30 && h->W == 16) launch_run<30, 16>(p, r, s);
-  else if (h->H == 16 && h->W == 30) launch_run<16, 30>(p, r, s);
-  else if (h->H == 8 && h->W == 8) launch_run<8, 8>(p, r, s);
-  else launch_run<0, 0>(p, r, s);
+  if (h->H == 16 && h->W == 16) launch_run<16, 16>(p, r, s, h->ev_start, h->ev_stop);
+  else if (h->H == 9 && h->W == 9) launch_run<9, 9>(p, r, s, h->ev_start, h->ev_stop);
+  else if (h->H == 30 && h->W == 16) launch_run<30, 16>(p, r, s, h->ev_start, h->ev_stop);
+  else if (h->H == 16 && h->W == 30) launch_run<16, 30>(p, r, s, h->ev_start, h->ev_stop);
+  else if (h->H == 8 && h->W == 8) launch_run<8, 8>(p, r, s, h->ev_start, h->ev_stop);
+  else launch_run<0, 0>(p, r, s, h->ev_start, h->ev_stop);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? MS_OK : hip_fail(e, "ms_run_tape launch");
 }

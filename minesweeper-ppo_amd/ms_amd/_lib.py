@@ -58,6 +58,10 @@ SIGNATURES = {
     # msenv_debug.h
     "ms_set_debug_flags": [_vp, ctypes.c_uint32],
     "ms_set_diag": [_vp, _vp],
+    "ms_set_timing_events": [_vp, _vp, _vp],
+    "ms_event_create": [ctypes.POINTER(_vp)],
+    "ms_event_elapsed_ms": [_vp, _vp, ctypes.POINTER(ctypes.c_float)],
+    "ms_event_destroy": [_vp],
 }
 MS_DBG_FORCE_SERIAL_PLACEMENT = 1
 _RESTYPES = {"ms_last_error": ctypes.c_char_p, "ms_abi_version": ctypes.c_int32}

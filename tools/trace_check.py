@@ -56,9 +56,10 @@ for p in pts:
     grid = 64 * n
     rl = p["roofline"]
     per_launch = rl["algo_bytes_per_launch"]
-    # the headline / point runs first in bench.py (warm-up + K steps); later dispatches of the
-    # same grid belong to other phases (the PPO rollout), so keep only the first warmup + K
-    ks = sorted(disp.get(("k_step", hw, grid), []))[:line["warmup"] + line["steps"]]
+    # the headline / point runs first in bench.py; later dispatches of the same grid belong to
+    # other phases (the PPO rollout), so keep only the config's own
+    # (warm-up + K graph steps + K dispatch-timed eager steps)
+    ks = sorted(disp.get(("k_step", hw, grid), []))[:line["warmup"] + 2 * line["steps"]]
     rec = {"board": board, "envs_per_gpu": n}
     if ks:
         dur = sum(d for _, d in ks) / len(ks) / 1e6  # ms

@@ -334,56 +334,6 @@ __device__ __forceinline__ void emit_obs(float* __restrict__ obs, uint8_t* __res
   }
 }
 
-// Workgroup-cooperative emit for boards whose cell count A is not a multiple of 4 (9x9:
-// 81): the EPW boards of a workgroup own EPW*10*A contiguous floats (12,960 B for 4 9x9
-// boards, 16-B aligned when the first board's index is a multiple of 4), so instead of one
-// dword store per cell and plane they leave as float4 stores of the whole block, every
-// lane of the workgroup taking a share. Each wave first writes its board's cell codes to
-// its LDS slice (sCodeAll[wave][A] bytes); one workgroup barrier; then lane t of the
-// workgroup writes float4s t, t + 64*EPW, ... of the block and u32s of the EPW*A-byte
-// mask block. Element f of the block is board f / (10A), plane (f % 10A) / A, cell f % A.
-template <int H_, int W_, int EPW>
-__device__ __forceinline__ void emit_obs_coop(float* __restrict__ obs, uint8_t* __restrict__ mask,
-                                              const uint64_t* sR, const uint64_t* sM, bool fc,
-                                              const Geo<H_, W_>& g, int lane, int wv,
-                                              uint8_t* sCodeAll, int code_stride) {
-  constexpr int A = H_ * W_;
-  constexpr int BA = 10 * A;  // floats per board
-  uint8_t* mine_codes = sCodeAll + wv * code_stride;
-  for (int i = lane; i < A; i += kWave) {
-    const int r = i / W_, c = i - r * W_;
-    mine_codes[i] = (uint8_t)cell_code(sR, sM, r, c, fc);
-  }
-  __syncthreads();
-  const int t = threadIdx.x;
-  if (obs) {
-    float4* o4 = reinterpret_cast<float4*>(obs);
-    for (int j = t; j < EPW * BA / 4; j += kWave * EPW) {
-      float v[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int f = 4 * j + k;
-        const int e = f / BA, rr = f - e * BA, ch = rr / A, i = rr - ch * A;
-        const uint32_t code = sCodeAll[e * code_stride + i];
-        v[k] = (ch == 0 ? code != 0u : code == (uint32_t)ch) ? 1.f : 0.f;
-      }
-      o4[j] = make_float4(v[0], v[1], v[2], v[3]);
-    }
-  }
-  if (mask) {
-    uint32_t* m4 = reinterpret_cast<uint32_t*>(mask);
-    for (int j = t; j < EPW * A / 4; j += kWave * EPW) {
-      uint32_t m = 0u;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int f = 4 * j + k, e = f / A, i = f - e * A;
-        m |= (sCodeAll[e * code_stride + i] ? 0u : 1u) << (8 * k);
-      }
-      m4[j] = m;
-    }
-  }
-}
-
 template <int H_, int W_>
 __device__ __forceinline__ void stage_rows(uint64_t* sR, uint64_t* sM, uint64_t rev, uint64_t mine,
                                            const Geo<H_, W_>& g, int lane) {
@@ -887,23 +837,8 @@ __global__ __launch_bounds__(64 * EPW) void k_step(KParams p) {
   // the obs stores are ~97 % of the bytes and the launch ends when they drain ----
   if (p.obs || p.mask) {
     stage_rows(sR, sM, rev, mine, g, lane);
-    // compile-time boards with A % 4 != 0 (9x9): the whole workgroup's block as float4s when
-    // every wave of the workgroup holds a live board and the outputs are aligned for it
-    // (a workgroup-uniform test, so the barrier inside is reached by all of its waves)
-    constexpr bool kCoop = EPW == 4 && H_ > 0 && W_ > 0 && ((H_ * W_) & 3) != 0;
-    bool coop = false;
-    if constexpr (kCoop) {
-      const int64_t base = (int64_t)blockIdx.x * EPW;
-      coop = base + EPW <= p.n && (reinterpret_cast<uintptr_t>(p.obs) & 15u) == 0 &&
-             (reinterpret_cast<uintptr_t>(p.mask) & 3u) == 0;
-      if (coop)
-        emit_obs_coop<H_, W_, EPW>(p.obs ? p.obs + base * 10 * A : nullptr, p.mask ? p.mask + base * A : nullptr,
-                                   sR, sM, fc, g, lane, wv, reinterpret_cast<uint8_t*>(&sTab_all[0][0]),
-                                   (int)sizeof(sTab_all[0]));
-    }
-    if (!coop)
-      emit_obs(p.obs ? p.obs + env * 10 * A : nullptr, p.mask ? p.mask + env * A : nullptr, sR, sM,
-               fc, g, lane, reinterpret_cast<uint8_t*>(sTab));
+    emit_obs(p.obs ? p.obs + env * 10 * A : nullptr, p.mask ? p.mask + env * A : nullptr, sR, sM,
+             fc, g, lane, reinterpret_cast<uint8_t*>(sTab));
   }
   // ---- persist state ----
   store_meta(mp, rng, step_count, fc, lane);

@@ -20,6 +20,11 @@ for v in ${VARIANTS:-base NO_DGRAD NO_EPI NO_P1LOAD NO_DYSTORE}; do
     python3 tools/fused_micro.py --no-torch --bwd ${EXP_ARGS:-} > /tmp/bv_$v.log 2>&1 || exit $?
   f=$(find /tmp/bv_$v -name "*kernel_stats.csv")
   echo "== $v" >> gpurun_out/bwd_variants.log
-  grep -E "k_bwd_data|k_wgrad|k_conv_gn_fwd" $f | awk -F'","' '{printf "%s avg_us=%.1f calls=%s\n", substr($1,2,60), $4/1000, $2}' >> gpurun_out/bwd_variants.log
+  python3 -c "
+import csv, sys
+for r in csv.DictReader(open('$f')):
+    if any(k in r['Name'] for k in ('k_bwd_data', 'k_wgrad', 'k_conv_gn_fwd')):
+        print(f\"{r['Name'][:70]} avg_us={float(r['AverageNs']) / 1e3:.1f} calls={r['Calls']}\")
+" >> gpurun_out/bwd_variants.log
 done
 cat gpurun_out/bwd_variants.log

@@ -53,21 +53,7 @@ struct BwdDataParams {
   __bf16* dx;
   float* part;  // [gridDim][3][96]
   int N, H, W;
-  int stagger;  // as FwdParams::stagger (mscnn.hip)
 };
-
-// Start delay of part of a persistent grid (10-ns ticks; > 0: the upper half of the
-// grid, < 0: the odd blocks): two co-resident workgroups running the same phase
-// sequence in lockstep contend for the matrix pipe and for HBM at the same time.
-__device__ __forceinline__ void stagger_start(int stagger) {
-  if (stagger == 0) return;
-  const bool late = stagger > 0 ? (int)blockIdx.x >= (int)gridDim.x / 2 : (blockIdx.x & 1) != 0;
-  const unsigned long long ticks = (unsigned long long)(stagger > 0 ? stagger : -stagger);
-  if (late) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
-  }
-}
 
 __host__ __device__ inline int dtile_bytes(int P) { return ((P + 1) * DCP * 2 + 15) & ~15; }
 __host__ __device__ constexpr int red_bytes() {  // sRed [PG][3][96] f32, aliased by sW [96][DCP] bf16
@@ -97,7 +83,6 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
     qr[t] = q < P ? q / W : -1000;  // an invalid pixel never lands on the board
     qc[t] = q < P ? q - qr[t] * W : -1000;
   }
-  stagger_start(p.stagger);
 
   for (int n = blockIdx.x; n < p.N; n += gridDim.x) {
     // loop-variant thread coordinates: keep the per-chunk address math inside the loop
@@ -136,16 +121,10 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
         mv[u] = 0u;
         if (i < NCH && gact && px < P) {
           const size_t o = ((size_t)n * P + px) * COUT + c8 * 8;
-#ifndef MC_EXP_B_NO_P1LOAD
           dv[u] = *reinterpret_cast<const u32x4*>(&p.dout[o]);
           if (RM) mv[u] = p.rmask[((size_t)n * P + px) * NC8 + c8];
           else ov[u] = *reinterpret_cast<const u32x4*>(&p.out[o]);
           yr[i] = *reinterpret_cast<const u32x4*>(&p.y[o]);
-#else
-          dv[u] = u32x4{(unsigned)o, 1u, 2u, 3u};
-          ov[u] = u32x4{(unsigned)o, 5u, 2u, 3u};
-          yr[i] = u32x4{(unsigned)o, 7u, 2u, 3u};
-#endif
         }
       }
 #pragma unroll
@@ -259,9 +238,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
           for (int j = 0; j < 8; ++j) d8[j] = (__bf16)(A[j] * (float)z8[j] + Bg * (float)y8[j] + Cg);
           const u32x4 v = __builtin_bit_cast(u32x4, d8);
           *reinterpret_cast<u32x4*>(&sD[px * DCP + c8 * 8]) = v;
-#ifndef MC_EXP_B_NO_DYSTORE
           *reinterpret_cast<u32x4*>(&p.dy[((size_t)n * P + px) * COUT + c8 * 8]) = v;
-#endif
         }
       }
     }
@@ -276,11 +253,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
       for (int ct = 0; ct < 3; ++ct)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[t][ct][i] = 0.f;
-#ifdef MC_EXP_B_NO_DGRAD
-    for (int tap = 0; tap < 0; ++tap) {
-#else
     for (int tap = 0; tap < 9; ++tap) {
-#endif
       if (tap + 1 < 9) {
         const u32x4* ws = reinterpret_cast<const u32x4*>(p.wT + (size_t)(tap + 1) * COUT * COUT);
 #pragma unroll
@@ -369,9 +342,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
           bf16x8 s8;
 #pragma unroll
           for (int j = 0; j < 8; ++j) s8[j] = (__bf16)((float)a8[j] + (float)r8[j]);
-#ifndef MC_EXP_B_NO_EPI
           *reinterpret_cast<u32x4*>(&p.dx[((size_t)n * P + px) * COUT + c8 * 8]) = __builtin_bit_cast(u32x4, s8);
-#endif
         }
       }
     }
@@ -390,7 +361,6 @@ struct WgradParams {
   const __bf16* x;
   float* part;  // [G][9][96][CIN]
   int N, H, W, G;
-  int stagger;
 };
 
 __host__ __device__ inline int wgrad_lds(int H, int W) {
@@ -554,7 +524,6 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams p) {
   const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
   const int cig = j % NCI, gid = (j / NCI) * 8 + xcd;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  stagger_start(p.stagger);
   switch (wave) {
     case 0: wgrad_body<CIN, 0, 7, PF>(p, sDY, sX, gid, cig * 32); break;
     case 1: wgrad_body<CIN, 7, 7, PF>(p, sDY, sX, gid, cig * 32); break;
@@ -673,10 +642,9 @@ void launch_wgrad_t(const WgradParams& p, int grid, size_t lds, hipStream_t s) {
 
 template <int CIN>
 void launch_wgrad(const WgradParams& p, int grid, size_t lds, hipStream_t s) {
-  // MC_WG_PF=0 turns the register prefetch of the 16x16 96-channel case off (A/B)
-  static const bool pf = getenv("MC_WG_PF") ? atoi(getenv("MC_WG_PF")) != 0 : true;
+  // 16x16 boards with 96 channels: the register prefetch of the next sample's dy and x slice
   if constexpr (CIN == 96) {
-    if (pf && p.H == 16 && p.W == 16) return launch_wgrad_t<CIN, true>(p, grid, lds, s);
+    if (p.H == 16 && p.W == 16) return launch_wgrad_t<CIN, true>(p, grid, lds, s);
   }
   launch_wgrad_t<CIN, false>(p, grid, lds, s);
 }
@@ -747,9 +715,6 @@ int mc_conv_gn_bwd(const uint16_t* dout, const uint16_t* out, const uint8_t* rel
   bp.N = n;
   bp.H = h;
   bp.W = w_;
-  static const int bstag = getenv("MC_BWD_STAGGER") ? atoi(getenv("MC_BWD_STAGGER")) : 0;
-  static const int wstag = getenv("MC_WG_STAGGER") ? atoi(getenv("MC_WG_STAGGER")) : 0;
-  bp.stagger = bstag;
   int rc = wT ? dispatch_bwd_data<true>(bp, pl.grid_d, s) : dispatch_bwd_data<false>(bp, pl.grid_d, s);
   if (rc) return rc;
   if ((rc = check_launch("k_bwd_data"))) return rc;
@@ -764,7 +729,6 @@ int mc_conv_gn_bwd(const uint16_t* dout, const uint16_t* out, const uint8_t* rel
   wp.H = h;
   wp.W = w_;
   wp.G = pl.G;
-  wp.stagger = wstag;
   const size_t lds = (size_t)wgrad_lds(h, w_);
   if (cin == 96) launch_wgrad<96>(wp, pl.grid_w, lds, s);
   else launch_wgrad<16>(wp, pl.grid_w, lds, s);

@@ -1485,7 +1485,7 @@ struct ms_handle {
   uint64_t* jump;  // [64][4] PCG64 jump-ahead table (device)
   uint64_t* diag;  // optional stamp buffer (MS_DIAG builds)
   uint32_t dbg_flags;
-  int epw;         // boards per workgroup of k_step (MSENV_EPW overrides, tools only)
+  int epw;         // boards per workgroup of k_step (4; generic shapes use 1)
   int late_on;     // ms_set_late_start called with prob > 0
   hipEvent_t ev_start, ev_stop;  // ms_set_timing_events (measurement only): stamp k_step / k_run
   LateCfg late;
@@ -1609,10 +1609,6 @@ int ms_create(const ms_cfg* cfg, int64_t n_total, uint64_t base_seed, int64_t en
   h->NW = (cfg->H + rpw - 1) / rpw;
   (void)hipGetDevice(&h->device);
   h->epw = 4;
-  if (const char* ev = getenv("MSENV_EPW")) {  // tools/ experiments only
-    const int v = atoi(ev);
-    if (v == 1 || v == 4) h->epw = v;
-  }
 
   // env.py:393-395: base = default_rng(seed); seeds = base.integers(0, 2**31-1, N)
   std::vector<EnvMeta> meta((size_t)env_count);

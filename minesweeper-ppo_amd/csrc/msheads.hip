@@ -172,44 +172,11 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams& p, HeadLds& 
   for (int ct = 0; ct < 6; ++ct) dw2acc[ct] = db1acc[ct] = 0.f;
 
   const int64_t ntiles = (p.M + TR - 1) / TR;
-  // the next tile's f rows and logit gradients are loaded into registers while this
-  // tile computes (one tile of HBM latency hidden per iteration)
   constexpr int NFC = TR * 12 / 256;
-#ifdef MC_HB_PREFETCH
-  u32x4 fv[NFC];
-  float dl0 = 0.f, dl1 = 0.f;
-#endif
-#define HB_LOAD(tile_)                                                                  \
-  do {                                                                                  \
-    const int64_t b_ = (tile_) * TR;                                                    \
-    _Pragma("unroll") for (int i_ = 0; i_ < NFC; ++i_) {                                \
-      const int c_ = tid + 256 * i_, r_ = c_ / 12, ch_ = c_ - r_ * 12;                  \
-      fv[i_] = u32x4{0u, 0u, 0u, 0u};                                                   \
-      if (b_ + r_ < p.M) fv[i_] = *reinterpret_cast<const u32x4*>(&p.f[(b_ + r_) * C + ch_ * 8]); \
-    }                                                                                   \
-    if (tid < TR) {                                                                     \
-      dl0 = b_ + tid < p.M ? p.dlp[b_ + tid] : 0.f;                                     \
-      dl1 = (b_ + tid < p.M && p.dlm) ? p.dlm[b_ + tid] : 0.f;                          \
-    }                                                                                   \
-  } while (0)
-#ifdef MC_HB_PREFETCH
-  if ((int64_t)blockIdx.x < ntiles) HB_LOAD((int64_t)blockIdx.x);
-#endif
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t base = tile * TR;
     const int zo = opaque0();
     // ---- stage f tile and the two logit gradients ----
-#ifdef MC_HB_PREFETCH
-#pragma unroll
-    for (int i = 0; i < NFC; ++i) {
-      const int c = tid + 256 * i + zo, r = c / 12, ch = c - r * 12;
-      *reinterpret_cast<u32x4*>(&L.f[sf_off(r, ch * 8)]) = fv[i];
-    }
-    if (tid < TR) {
-      L.dl[0][tid] = dl0;
-      L.dl[1][tid] = dl1;
-    }
-#else
     // (prefetching the next tile here needs ~26 more VGPRs than the kernel has: spills)
     // every load is issued unconditionally from a clamped row and masked afterwards:
     // a guarded load sits in its own exec branch with its own vmcnt(0), one round
@@ -237,11 +204,7 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams& p, HeadLds& 
         L.dl[1][tid] = ok ? d1 : 0.f;
       }
     }
-#endif
     __syncthreads();
-#ifdef MC_HB_PREFETCH
-    if (tile + gridDim.x < ntiles) HB_LOAD(tile + gridDim.x);
-#endif
     // ---- recompute H[px][c] for this wave's 32 rows ----
     {
       f32x16 acc[6];
@@ -357,7 +320,6 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams& p, HeadLds& 
     }
     __syncthreads();  // f / dh images are re-staged by the next tile
   }
-#undef HB_LOAD
   // ---- partials ----
   float* part = p.part + (size_t)blockIdx.x * PART;
 #pragma unroll

@@ -31,12 +31,10 @@ def _ref(x, w, b, g, be, H, W, res=None, dmask=None):
 @pytest.mark.parametrize("H,W,cin,n", [(16, 16, 96, 300), (16, 16, 16, 37), (9, 9, 96, 70), (30, 16, 96, 20),
                                        (16, 30, 96, 9), (5, 7, 16, 3)])
 @pytest.mark.parametrize("with_res", [False, True])
-@pytest.mark.parametrize("rw", ["0", "1"])
-def test_conv_gn_fwd_matches_torch(gpu, H, W, cin, n, with_res, rw, monkeypatch):
-    """rw=1: the resident-weight kernel (96-channel layers on <= 256 cells, MC_FWD_RW=1);
-    rw=0: the per-sample weight-staging kernel (the default)."""
+def test_conv_gn_fwd_matches_torch(gpu, H, W, cin, n, with_res):
+    """The fused forward (conv + bias + GroupNorm + affine [+ residual] + ReLU [+ dropout
+    scale]) and its ReLU bitmask vs a torch fp32 reference of the same op."""
     from ms_amd.fused import conv_gn_fwd, prep_weight
-    monkeypatch.setenv("MC_FWD_RW", rw)
     torch.manual_seed(0)
     P = H * W
     x = (torch.randn(n, P, cin, device=gpu) * (0.5 if cin == 96 else 1.0)).to(torch.bfloat16)

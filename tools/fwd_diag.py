@@ -41,7 +41,7 @@ d = d[d.sum(1) > 0].double()
 grid = d.shape[0]
 per_sample = d.sum(0) / n * grid / grid  # ticks per sample (each WG processes n/grid samples)
 per_wg_sample = d.mean(0) / (n / grid)
-names = ["stage+w0", "9 taps", "GN stats", "y->LDS", "scale+out", "tail sync"] if os.environ.get("MC_FWD_RW") == "0" else ["stage", "27 k-steps", "stats p0", "stats p1+y", "epilogue", "tail sync"]
+names = ["stage+w0", "9 taps", "GN stats", "y->LDS", "scale+out", "tail sync"]
 print(f"grid {grid} workgroups, {n / grid:.1f} samples each; ticks per sample per workgroup:")
 tot = 0.0
 for i, nm in enumerate(names):

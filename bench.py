@@ -212,6 +212,28 @@ GFLOP_FWD_16, GFLOP_FWDBWD_16 = 0.4388, 1.3073
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16
 
 
+def ppo_kernel_profile():
+    """The PPO minibatch's trunk kernels at N = 32,768 from the committed rocprofv3 passes
+    (tools/profile_round.sh step 3 -> profiles/r*/pmc_ppo_minibatch_32768.json): mean
+    launch time, HBM bytes per launch (FETCH_SIZE doubled for 16-B/lane streams + WRITE_SIZE),
+    MFMA-busy fraction and TFLOP/s on the 2*N*P*96*96*9 algorithmic flops of a 96->96 layer."""
+    import glob
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_ppo_minibatch_32768.json")))
+    if not cands:
+        return None
+    d = json.load(open(cands[-1]))
+    out = {"source": os.path.relpath(cands[-1], ROOT)}
+    for name, k in d["kernels"].items():
+        short = name.split("(anonymous namespace)::", 1)[-1].split("((anonymous")[0]
+        if short in out or "achieved_TFLOPs" not in k:
+            continue
+        out[short] = {"mean_us": k["mean_us"], "traffic_bytes_per_launch": k["traffic_bytes"],
+                      "hbm_frac": k["traffic_bytes"] / (k["mean_us"] * 1e-6) / (HBM_PEAK_GBS * 1e9),
+                      "mfma_busy": k.get("mfma_busy_frac"), "achieved_TFLOPs": k["achieved_TFLOPs"],
+                      "mfma_frac": k["mfma_frac_of_2500"]}
+    return out
+
+
 def ppo_bench(args, world, rank, local_rank, dev):
     """Combined rollout + GAE + PPO-update loop (BASELINE metric, 2nd half):
     configs/16x16x40_medium.yaml with num_envs = envs_per_gpu * world (global),
@@ -245,6 +267,8 @@ def ppo_bench(args, world, rank, local_rank, dev):
     n_loc, T = args.envs, cfg.steps_per_env
     gflop = (T * n_loc * GFLOP_FWD_16 + n_loc * GFLOP_FWD_16 + cfg.ppo_epochs * T * n_loc * GFLOP_FWDBWD_16)
     mean = lambda k: float(np.mean([p[k] for p in prof]))  # noqa: E731
+    kprof = ppo_kernel_profile()
+    dom = max((k for k in (kprof or {}) if k != "source"), key=lambda k: kprof[k]["mean_us"], default=None)
     return {"metric": "PPO updates/sec (combined rollout + GAE + 3x8 minibatch update)",
             "updates_per_s": 1.0 / spu, "s_per_update": spu,
             "samples_per_s": n_loc * world * T / spu, "envs_total": n_loc * world, "steps_per_env": T,
@@ -252,7 +276,9 @@ def ppo_bench(args, world, rank, local_rank, dev):
             "amp": args.amp, "model": "cnn_residual 96ch x 5 blocks (950,947 params)",
             "roofline": {"bound": "mfma", "achieved": gflop / spu / 1e3, "peak": BF16_DENSE_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": gflop / spu / 1e3 / BF16_DENSE_PEAK_TFLOPS,
-                         "traffic": None, "algo_gflop_per_update_per_gpu": gflop},
+                         "traffic": kprof[dom]["traffic_bytes_per_launch"] if dom else None,
+                         "traffic_kernel": dom, "traffic_unit": "HBM bytes per launch at N=32768",
+                         "algo_gflop_per_update_per_gpu": gflop, "trunk_kernels": kprof},
             "loss": prof[-1].get("loss"), "entropy": prof[-1].get("entropy")}
 
 
@@ -333,27 +359,37 @@ def env_bench(args, world, rank, dev, H, W, K, n_local, multistep=True):
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
-    # Dominant-kernel duration: after the timed region, K more eager steps whose k_step
-    # dispatches stamp their own HIP events (hipExtLaunchKernel via ms_set_timing_events),
-    # i.e. each launch's execution time as rocprofv3's kernel trace reports it (the per-step
-    # time above additionally holds k_tape and the launch boundaries).
+    # Dominant-kernel duration from HIP events on the launch stream: the span of the K-step
+    # graph minus the span of a graph holding only its K tape launches, divided by K = what
+    # one ms_step adds to a step, launch boundary included. (Dispatch-stamped events, used
+    # for k_run, read high on a launch this short: the start stamp is taken while the
+    # preceding k_tape is still running. tools/trace_check.py compares both against the
+    # rocprofv3 trace of the same run.)
+    if graph is not None:
+        gt = capture(True)
+        ev_full = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev_tape = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        # the step graph is replayed once more for the span: the boards move on, the work per
+        # step is statistically the same
+        ev_full[0].record()
+        graph.replay()
+        ev_full[1].record()
+        ev_tape[0].record()
+        gt.replay()
+        ev_tape[1].record()
+        torch.cuda.synchronize()
+        kern_ms = (ev_full[0].elapsed_time(ev_full[1]) - ev_tape[0].elapsed_time(ev_tape[1])) / args.steps
+        kern_method = "graph span difference (tape+step vs tape only) / K"
+        del gt
+    else:
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        for k in range(args.steps):
+            one_step(args.warmup + args.steps + k, sp, evs[k])
+        torch.cuda.synchronize()
+        kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        kern_method = "events around each ms_step (eager)"
     del graph
-    graph = None
-    n_t = args.steps
-    timer = DispatchTimer(lib, L, h, n_t)
-    for k in range(n_t):
-        L.check(lib.ms_tape_actions(h, args.warmup + args.steps + k, args.tape, ptrs[0], sp))
-        pt = list(ptrs)
-        if not args.diag_no_obs:
-            t_ = args.warmup + args.steps + k
-            pt[1], pt[2] = L.ptr(obs_ring[t_ % R]), L.ptr(mask_ring[t_ % R])
-        timer.arm(k)
-        L.check(lib.ms_step(h, *pt, sp))
-    timer.disarm()
-    torch.cuda.synchronize()
-    kern_ms = float(np.mean([timer.elapsed_ms(k) for k in range(n_t)]))
-    timer.close()
-    kern_method = "mean of dispatch-stamped HIP events (hipExtLaunchKernel) over K eager k_step launches"
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

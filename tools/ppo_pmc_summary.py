@@ -57,7 +57,10 @@ for k, ds in dur.items():
            "fetch_doubled": wide}
     if k in mb and gui.get(k):
         rec["mfma_busy_frac"] = mb[k] / (gui[k] / 8.0 * 1024.0)
-    if ("<96" in k or "96," in k) and any(t in k for t in ("k_conv_gn_fwd", "k_bwd_data", "k_wgrad")):
+    # the 96 -> 96 layers: forward / wgrad instantiated for 96 input channels, k_bwd_data's
+    # data-gradient variant (template argument DGRAD = true; the stem's has no dgrad)
+    if ("k_conv_gn_fwd<96" in k or "k_wgrad<96" in k or "k_bwd_data<2, true" in k or "k_bwd_data<1, true" in k
+            or "k_bwd_data<3, true" in k or "k_bwd_data<4, true" in k):
         rec["algo_tflop"] = flops96 / 1e12
         rec["achieved_TFLOPs"] = flops96 / (us * 1e-6) / 1e12
         rec["mfma_frac_of_2500"] = rec["achieved_TFLOPs"] / 2500.0

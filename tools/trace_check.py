@@ -59,7 +59,7 @@ for p in pts:
     # the headline / point runs first in bench.py; later dispatches of the same grid belong to
     # other phases (the PPO rollout), so keep only the config's own
     # (warm-up + K graph steps + K dispatch-timed eager steps)
-    ks = sorted(disp.get(("k_step", hw, grid), []))[:line["warmup"] + 2 * line["steps"]]
+    ks = sorted(disp.get(("k_step", hw, grid), []))[:line["warmup"] + 2 * line["steps"]]  # warm-up, timed graph, span graph
     rec = {"board": board, "envs_per_gpu": n}
     if ks:
         dur = sum(d for _, d in ks) / len(ks) / 1e6  # ms

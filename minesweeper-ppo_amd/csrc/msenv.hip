@@ -1704,7 +1704,7 @@ int ms_event_elapsed_ms(void* start_event, void* stop_event, float* ms) {
 }
 
 int ms_event_destroy(void* event) {
-  if (event) hipEventDestroy((hipEvent_t)event);
+  if (event) (void)hipEventDestroy((hipEvent_t)event);
   return MS_OK;
 }
 

@@ -6,8 +6,12 @@
  * -> [Dropout2d] of one stem / half-block (cnn_residual.py:10-26, 50-54) with
  * one MFMA implicit-GEMM kernel per sample-workgroup, and its backward.
  *
- * Layouts: activations NHWC bf16 [N][H*W][C]; conv weights bf16 [9][COUT][CIN]
+ * Layouts: activations NHWC [N][H*W][C]; conv weights [9][COUT][CIN]
  * (tap-major, tap = 3*(dy+1) + (dx+1)); per-channel params f32. COUT = 96.
+ * Activations, weights and their gradients are 16-bit, of the type `dtype` names:
+ * MC_DTYPE_BF16 (bf16 autocast) or MC_DTYPE_F16 (fp16 autocast, the reference's own
+ * training precision, ppo.py:25); every sum and statistic is f32 either way.
+ * Below, "bf16" means that 16-bit type.
  * All pointers are device pointers; `stream` is a hipStream_t (void*).
  * Returns 0 on success, MS_EINVAL / MS_EHIP (msenv.h) otherwise.
  */
@@ -20,6 +24,9 @@
 extern "C" {
 #endif
 
+#define MC_DTYPE_BF16 0
+#define MC_DTYPE_F16 1
+
 /* Forward of one fused layer:
  *   y   = conv3x3(x, w) + bias                       (saved to ysave, bf16)
  *   out = relu(GN(y) * gamma + beta [+ res]) [* dmask[n][c]]
@@ -31,7 +38,7 @@ extern "C" {
 int mc_conv_gn_fwd(const uint16_t* x, const uint16_t* w, const float* bias, const float* gamma,
                    const float* beta, const uint16_t* res, const float* dmask, uint16_t* out,
                    uint16_t* ysave, float* stats, uint8_t* relu_mask, int32_t n, int32_t h, int32_t w_,
-                   int32_t cin, float eps, void* stream);
+                   int32_t cin, float eps, int32_t dtype, void* stream);
 
 /* Backward of one fused layer (the forward above with the same n, h, w, cin).
  * Inputs: dout = dL/d(out); out (or its relu_mask; the other may be NULL), ysave, stats
@@ -52,7 +59,7 @@ int mc_conv_gn_bwd(const uint16_t* dout, const uint16_t* out, const uint8_t* rel
                    const float* gamma, const float* dmask, const uint16_t* x, const uint16_t* wT,
                    const uint16_t* addend, uint16_t* dy, uint16_t* dz, uint16_t* dx, float* dw, float* dgn,
                    float* work, int64_t work_floats, int32_t n, int32_t h, int32_t w_, int32_t cin,
-                   void* stream);
+                   int32_t dtype, void* stream);
 
 /* f32 elements of scratch mc_conv_gn_bwd needs for these sizes. */
 int64_t mc_conv_gn_bwd_workspace(int32_t n, int32_t h, int32_t w_, int32_t cin);
@@ -62,7 +69,7 @@ int64_t mc_conv_gn_bwd_workspace(int32_t n, int32_t h, int32_t w_, int32_t cin);
  * w1: bf16 [nh*96][96] (policy rows first, then mine), b1/w2: f32 [nh*96], b2: f32 [nh].
  * out_m == NULL computes the policy head only (nh = 1). Logits are f32 [M]. */
 int mc_heads_fwd(const uint16_t* f, const uint16_t* w1, const float* b1, const float* w2, const float* b2,
-                 float* out_p, float* out_m, int64_t M, void* stream);
+                 float* out_p, float* out_m, int64_t M, int32_t dtype, void* stream);
 
 /* Backward of both heads. dlp/dlm: f32 [M] logit gradients (dlm may be NULL = 0).
  * w1pT: bf16 [96][96] = policy W1 transposed. df (bf16 [M][96]) = policy-head input
@@ -70,7 +77,8 @@ int mc_heads_fwd(const uint16_t* f, const uint16_t* w1, const float* b1, const f
  * dw1: f32 [192][96], db1, dw2: f32 [192]. work: mc_heads_bwd_workspace(M) floats. */
 int mc_heads_bwd(const uint16_t* f, const float* dlp, const float* dlm, const uint16_t* w1, const uint16_t* w1pT,
                  const float* b1, const float* w2, const float* gadd, int32_t P, uint16_t* df, float* dw1,
-                 float* db1, float* dw2, float* work, int64_t work_floats, int64_t M, void* stream);
+                 float* db1, float* dw2, float* work, int64_t work_floats, int64_t M, int32_t dtype,
+                 void* stream);
 int64_t mc_heads_bwd_workspace(int64_t M);
 
 /* Thread-local message of the last failing mc_* call. */

@@ -48,16 +48,17 @@ namespace {
 
 using namespace mc;
 
+template <typename E>
 struct FwdParams {
-  const __bf16* x;
-  const __bf16* wt;
+  const E* x;
+  const E* wt;
   const float* bias;
   const float* gamma;
   const float* beta;
-  const __bf16* res;
+  const E* res;
   const float* dmask;
-  __bf16* out;
-  __bf16* ysave;
+  E* out;
+  E* ysave;
   float* stats;
   uint8_t* rmask;  // optional ReLU bitmask [N][P][12]: bit j of byte (px, c8) = out[px][8*c8 + j] > 0
   int N, H, W;
@@ -122,17 +123,18 @@ __host__ __device__ inline int region0_elems(int H, int W) {
 
 // Two workgroups per CU (~75 KB of LDS each) cover one another's barriers and epilogues;
 // nothing is held in registers across phases.
-template <int CIN, int NPT, bool FULL>
-__global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams p) {
+template <typename E, int CIN, int NPT, bool FULL>
+__global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams<E> p) {
+  typedef typename EV<E>::v8 E8;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int CINP = cinp<CIN>();
   constexpr int C8 = CIN / 8;
   constexpr int NPF = (NPT * 128 * C8 + 255) / 256;  // 16-B input chunks per thread
   constexpr int NWC = (COUT * C8 + 255) / 256;        // 16-B weight chunks per thread and tap
   const int H = p.H, W = p.W, P = H * W;
-  __bf16* sX = reinterpret_cast<__bf16*>(smem);
-  __bf16* sO = sX;
-  __bf16* sW = sX + region0_elems<CIN>(H, W);
+  E* sX = reinterpret_cast<E*>(smem);
+  E* sO = sX;
+  E* sW = sX + region0_elems<CIN>(H, W);
   float* sRed = reinterpret_cast<float*>(sW + COUT * CINP);
   float* sGB = sRed + WAVES * NGRP;  // [gamma | beta]
   float* sAB = sGB + 2 * COUT;        // per sample: [scale | shift | dropout scale]
@@ -199,13 +201,13 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
       // issued before step k's MFMAs (left alone, the scheduler reuses one operand set
       // and waits on every read)
       constexpr int KS = CIN / 16;
-      bf16x8 A[2][NPT], B[2][3];
-      auto ld = [&](int ks, bf16x8 (&a)[NPT], bf16x8 (&b)[3]) {
+      E8 A[2][NPT], B[2][3];
+      auto ld = [&](int ks, E8 (&a)[NPT], E8 (&b)[3]) {
 #pragma unroll
         for (int ct = 0; ct < 3; ++ct)
-          b[ct] = *reinterpret_cast<const bf16x8*>(&sW[(ct * 32 + l32) * CINP + ks * 16 + 8 * hh]);
+          b[ct] = *reinterpret_cast<const E8*>(&sW[(ct * 32 + l32) * CINP + ks * 16 + 8 * hh]);
 #pragma unroll
-        for (int t = 0; t < NPT; ++t) a[t] = *reinterpret_cast<const bf16x8*>(&sX[aoff[t] + ks * 16]);
+        for (int t = 0; t < NPT; ++t) a[t] = *reinterpret_cast<const E8*>(&sX[aoff[t] + ks * 16]);
       };
       ld(0, A[0], B[0]);
       __builtin_amdgcn_sched_group_barrier(0x100, NPT + 3, 0);
@@ -219,7 +221,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
         for (int t = 0; t < NPT; ++t)
 #pragma unroll
           for (int ct = 0; ct < 3; ++ct)
-            acc[t][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[ks & 1][t], B[ks & 1][ct], acc[t][ct], 0, 0, 0);
+            acc[t][ct] = mfma32(A[ks & 1][t], B[ks & 1][ct], acc[t][ct]);
         __builtin_amdgcn_sched_group_barrier(0x008, 3 * NPT, 0);
       }
       __syncthreads();  // sW (and after the last tap sX) fully read
@@ -299,7 +301,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int px = (wave * NPT + t) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          if (FULL || px < P) sO[px * COUT + ct * 32 + l32] = (__bf16)(acc[t][ct][i] + biasv[ct]);
+          if (FULL || px < P) sO[px * COUT + ct * 32 + l32] = (E)(acc[t][ct][i] + biasv[ct]);
         }
     FSTAMP(3);  // y -> LDS
     if (tid < COUT) {  // z = y * scale + shift (+ res), then ReLU, then * dropout scale
@@ -353,14 +355,14 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
         const size_t o = (size_t)n * P * COUT + (size_t)c * 8;
         const u32x4 yv = *reinterpret_cast<const u32x4*>(&sO[c * 8]);
         if (p.ysave) *reinterpret_cast<u32x4*>(&p.ysave[o]) = yv;
-        const bf16x8 y8 = __builtin_bit_cast(bf16x8, yv);
-        const bf16x8 r8 = __builtin_bit_cast(bf16x8, rq[k % RB]);
-        bf16x8 o8;
+        const E8 y8 = __builtin_bit_cast(E8, yv);
+        const E8 r8 = __builtin_bit_cast(E8, rq[k % RB]);
+        E8 o8;
         uint32_t mb = 0u;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float z = fmaxf((float)y8[j] * ca[k % 3][j] + cb[k % 3][j] + (float)r8[j], 0.f);
-          o8[j] = (__bf16)(z * cd[k % 3][j]);
+          o8[j] = (E)(z * cd[k % 3][j]);
           mb |= ((float)o8[j] > 0.f ? 1u : 0u) << j;
         }
         *reinterpret_cast<u32x4*>(&p.out[o]) = __builtin_bit_cast(u32x4, o8);
@@ -377,8 +379,8 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
 #endif
 }
 
-template <int CIN, int NPT, bool FULL>
-int launch_fwd(const FwdParams& p, hipStream_t s) {
+template <typename E, int CIN, int NPT, bool FULL>
+int launch_fwd(const FwdParams<E>& p, hipStream_t s) {
   constexpr int CINP = cinp<CIN>();
   const size_t lds = (size_t)region0_elems<CIN>(p.H, p.W) * 2 + (size_t)COUT * CINP * 2 + WAVES * NGRP * 4 +
                      5 * COUT * 4;
@@ -388,14 +390,14 @@ int launch_fwd(const FwdParams& p, hipStream_t s) {
   }
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k_conv_gn_fwd<CIN, NPT, FULL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)k_conv_gn_fwd<E, CIN, NPT, FULL>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     attr_set = true;
   }
   const int per_cu = lds <= 80 * 1024 ? 2 : 1;
   const int cap = per_cu * num_cus();
   const int grid = p.N < cap ? p.N : cap;
-  hipLaunchKernelGGL((k_conv_gn_fwd<CIN, NPT, FULL>), dim3(grid), dim3(256), lds, s, p);
+  hipLaunchKernelGGL((k_conv_gn_fwd<E, CIN, NPT, FULL>), dim3(grid), dim3(256), lds, s, p);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd launch: %s", hipGetErrorString(e));
@@ -404,17 +406,17 @@ int launch_fwd(const FwdParams& p, hipStream_t s) {
   return MS_OK;
 }
 
-template <int CIN>
-int dispatch_fwd(const FwdParams& p, hipStream_t s) {
+template <typename E, int CIN>
+int dispatch_fwd(const FwdParams<E>& p, hipStream_t s) {
   const int P = p.H * p.W;
   const int tiles = (P + 31) / 32;
   const int npt = (tiles + WAVES - 1) / WAVES;
-  if (P == 256) return launch_fwd<CIN, 2, true>(p, s);
+  if (P == 256) return launch_fwd<E, CIN, 2, true>(p, s);
   switch (npt) {
-    case 1: return launch_fwd<CIN, 1, false>(p, s);
-    case 2: return launch_fwd<CIN, 2, false>(p, s);
-    case 3: return launch_fwd<CIN, 3, false>(p, s);
-    case 4: return launch_fwd<CIN, 4, false>(p, s);
+    case 1: return launch_fwd<E, CIN, 1, false>(p, s);
+    case 2: return launch_fwd<E, CIN, 2, false>(p, s);
+    case 3: return launch_fwd<E, CIN, 3, false>(p, s);
+    case 4: return launch_fwd<E, CIN, 4, false>(p, s);
     default:
       snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd: %d pixels > 512 unsupported", P);
       return MS_EINVAL;
@@ -427,6 +429,37 @@ int dispatch_fwd(const FwdParams& p, hipStream_t s) {
 unsigned long long* g_fwd_diag = nullptr;
 #endif
 
+namespace {
+
+template <typename E>
+int run_fwd(const uint16_t* x, const uint16_t* w, const float* bias, const float* gamma, const float* beta,
+            const uint16_t* res, const float* dmask, uint16_t* out, uint16_t* ysave, float* stats, uint8_t* relu_mask,
+            int32_t n, int32_t h, int32_t w_, int32_t cin, float eps, hipStream_t s) {
+  FwdParams<E> p;
+  p.x = reinterpret_cast<const E*>(x);
+  p.wt = reinterpret_cast<const E*>(w);
+  p.bias = bias;
+  p.gamma = gamma;
+  p.beta = beta;
+  p.res = reinterpret_cast<const E*>(res);
+  p.dmask = dmask;
+  p.out = reinterpret_cast<E*>(out);
+  p.ysave = reinterpret_cast<E*>(ysave);
+  p.stats = stats;
+  p.rmask = relu_mask;
+  p.N = n;
+  p.H = h;
+  p.W = w_;
+  p.eps = eps;
+  p.diag = nullptr;
+#ifdef MC_DIAG
+  p.diag = g_fwd_diag;
+#endif
+  return cin == 16 ? dispatch_fwd<E, 16>(p, s) : dispatch_fwd<E, 96>(p, s);
+}
+
+}  // namespace
+
 extern "C" {
 
 const char* mc_last_error(void) { return g_err; }
@@ -438,35 +471,20 @@ void mc_set_fwd_diag(unsigned long long* d) { g_fwd_diag = d; }
 
 int mc_conv_gn_fwd(const uint16_t* x, const uint16_t* w, const float* bias, const float* gamma, const float* beta,
                    const uint16_t* res, const float* dmask, uint16_t* out, uint16_t* ysave, float* stats,
-                   uint8_t* relu_mask, int32_t n, int32_t h, int32_t w_, int32_t cin, float eps, void* stream) {
+                   uint8_t* relu_mask, int32_t n, int32_t h, int32_t w_, int32_t cin, float eps, int32_t dtype,
+                   void* stream) {
   if (!x || !w || !bias || !gamma || !beta || !out || n <= 0 || h <= 0 || w_ <= 0) {
     snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd: bad argument");
     return MS_EINVAL;
   }
-  FwdParams p;
-  p.x = reinterpret_cast<const __bf16*>(x);
-  p.wt = reinterpret_cast<const __bf16*>(w);
-  p.bias = bias;
-  p.gamma = gamma;
-  p.beta = beta;
-  p.res = reinterpret_cast<const __bf16*>(res);
-  p.dmask = dmask;
-  p.out = reinterpret_cast<__bf16*>(out);
-  p.ysave = reinterpret_cast<__bf16*>(ysave);
-  p.stats = stats;
-  p.rmask = relu_mask;
-  p.N = n;
-  p.H = h;
-  p.W = w_;
-  p.eps = eps;
-  p.diag = nullptr;
-#ifdef MC_DIAG
-  p.diag = g_fwd_diag;
-#endif
+  if (cin != 16 && cin != 96) {
+    snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd: cin %d unsupported (16 or 96)", cin);
+    return MS_EINVAL;
+  }
   hipStream_t s = (hipStream_t)stream;
-  if (cin == 16) return dispatch_fwd<16>(p, s);
-  if (cin == 96) return dispatch_fwd<96>(p, s);
-  snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd: cin %d unsupported (16 or 96)", cin);
+  if (dtype == MC_DT_BF16) return run_fwd<__bf16>(x, w, bias, gamma, beta, res, dmask, out, ysave, stats, relu_mask, n, h, w_, cin, eps, s);
+  if (dtype == MC_DT_F16) return run_fwd<_Float16>(x, w, bias, gamma, beta, res, dmask, out, ysave, stats, relu_mask, n, h, w_, cin, eps, s);
+  snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd: dtype %d unsupported (0 bf16, 1 f16)", dtype);
   return MS_EINVAL;
 }
 

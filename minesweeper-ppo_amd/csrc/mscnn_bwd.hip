@@ -38,19 +38,20 @@ constexpr int DCP = 104;       // dy tile row stride (elements): conflict-free d
 constexpr int PG = 21;         // pixel groups of the element-wise passes: thread = (pg, c8)
 constexpr int NC8 = COUT / 8;  // 16-byte chunks per 96-channel pixel row
 
+template <typename E>
 struct BwdDataParams {
-  const __bf16* dout;
-  const __bf16* out;
+  const E* dout;
+  const E* out;
   const uint8_t* rmask;  // ReLU bitmask of the forward (replaces the sign test on out), or NULL
-  const __bf16* y;
+  const E* y;
   const float* stats;
   const float* gamma;
   const float* dmask;
-  const __bf16* wT;
-  const __bf16* addend;
-  __bf16* dy;
-  __bf16* dz;
-  __bf16* dx;
+  const E* wT;
+  const E* addend;
+  E* dy;
+  E* dz;
+  E* dx;
   float* part;  // [gridDim][3][96]
   int N, H, W;
 };
@@ -62,13 +63,14 @@ __host__ __device__ constexpr int red_bytes() {  // sRed [PG][3][96] f32, aliase
 __host__ __device__ inline int bwd_data_lds(int P) { return dtile_bytes(P) + red_bytes() + 6 * COUT * 4; }
 
 // RM: the ReLU decisions come from the forward's bitmask (p.rmask), else from out
-template <int NPT, bool DGRAD, int NCH, bool RM>
-__global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParams p) {
+template <typename E, int NPT, bool DGRAD, int NCH, bool RM>
+__global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParams<E> p) {
+  typedef typename EV<E>::v8 E8;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int H = p.H, W = p.W, P = H * W;
-  __bf16* sD = reinterpret_cast<__bf16*>(smem);  // [P+1][DCP] (row P = 0); later [P][96] dx staging
+  E* sD = reinterpret_cast<E*>(smem);  // [P+1][DCP] (row P = 0); later [P][96] dx staging
   float* sRed = reinterpret_cast<float*>(smem + dtile_bytes(P));
-  __bf16* sW = reinterpret_cast<__bf16*>(sRed);  // W^T[tap] as [ci][DCP]
+  E* sW = reinterpret_cast<E*>(sRed);  // W^T[tap] as [ci][DCP]
   float* sCo = reinterpret_cast<float*>(smem + dtile_bytes(P) + red_bytes());  // [3][96]
   float* sTmp = sCo + 3 * COUT;                                                 // [2][96]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hh = lane >> 5;
@@ -131,19 +133,19 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
       for (int u = 0; u < LB; ++u) {
         const int i = i0 + u, px = pg + PG * i;
         if (i < NCH && gact && px < P) {
-          const bf16x8 d8 = __builtin_bit_cast(bf16x8, dv[u]);
-          const bf16x8 y8 = __builtin_bit_cast(bf16x8, yr[i]);
+          const E8 d8 = __builtin_bit_cast(E8, dv[u]);
+          const E8 y8 = __builtin_bit_cast(E8, yr[i]);
           uint32_t pos = mv[u];
           if (!RM) {
-            const bf16x8 o8 = __builtin_bit_cast(bf16x8, ov[u]);
+            const E8 o8 = __builtin_bit_cast(E8, ov[u]);
 #pragma unroll
             for (int j = 0; j < 8; ++j) pos |= ((float)o8[j] > 0.f ? 1u : 0u) << j;
           }
-          bf16x8 z8;
+          E8 z8;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const float d = (float)d8[j] * dm[j];
-            z8[j] = (__bf16)(((pos >> j) & 1u) ? d : 0.f);
+            z8[j] = (E)(((pos >> j) & 1u) ? d : 0.f);
             const float zf = (float)z8[j];
             const float yh = ((float)y8[j] - mean) * rstd;
             s1[j] += zf;
@@ -231,11 +233,11 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
           // dz is stored here rather than in pass 1: a store there would sit between the
           // next chunk batch's loads and their use, and vmcnt would drain it each batch
           if (p.dz) *reinterpret_cast<u32x4*>(&p.dz[((size_t)n * P + px) * COUT + c8 * 8]) = zv;
-          const bf16x8 z8 = __builtin_bit_cast(bf16x8, zv);
-          const bf16x8 y8 = __builtin_bit_cast(bf16x8, yr[i]);
-          bf16x8 d8;
+          const E8 z8 = __builtin_bit_cast(E8, zv);
+          const E8 y8 = __builtin_bit_cast(E8, yr[i]);
+          E8 d8;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) d8[j] = (__bf16)(A[j] * (float)z8[j] + Bg * (float)y8[j] + Cg);
+          for (int j = 0; j < 8; ++j) d8[j] = (E)(A[j] * (float)z8[j] + Bg * (float)y8[j] + Cg);
           const u32x4 v = __builtin_bit_cast(u32x4, d8);
           *reinterpret_cast<u32x4*>(&sD[px * DCP + c8 * 8]) = v;
           *reinterpret_cast<u32x4*>(&p.dy[((size_t)n * P + px) * COUT + c8 * 8]) = v;
@@ -272,20 +274,20 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
       }
       // 6 ci steps, operands double-buffered: step k+1's LDS reads are issued before
       // step k's MFMAs
-      auto ld = [&](int k0, bf16x8 (&a)[NPT], bf16x8 (&b)[3]) {
+      auto ld = [&](int k0, E8 (&a)[NPT], E8 (&b)[3]) {
 #pragma unroll
         for (int ct = 0; ct < 3; ++ct)
-          b[ct] = *reinterpret_cast<const bf16x8*>(&sW[(ct * 32 + l32) * DCP + k0 + 8 * hh]);
+          b[ct] = *reinterpret_cast<const E8*>(&sW[(ct * 32 + l32) * DCP + k0 + 8 * hh]);
 #pragma unroll
-        for (int t = 0; t < NPT; ++t) a[t] = *reinterpret_cast<const bf16x8*>(&sD[aoff[t] + k0]);
+        for (int t = 0; t < NPT; ++t) a[t] = *reinterpret_cast<const E8*>(&sD[aoff[t] + k0]);
       };
-      auto mm = [&](const bf16x8 (&a)[NPT], const bf16x8 (&b)[3]) {
+      auto mm = [&](const E8 (&a)[NPT], const E8 (&b)[3]) {
 #pragma unroll
         for (int t = 0; t < NPT; ++t)
 #pragma unroll
-          for (int ct = 0; ct < 3; ++ct) acc[t][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t], b[ct], acc[t][ct], 0, 0, 0);
+          for (int ct = 0; ct < 3; ++ct) acc[t][ct] = mfma32(a[t], b[ct], acc[t][ct]);
       };
-      bf16x8 a0[NPT], b0[3], a1[NPT], b1[3];
+      E8 a0[NPT], b0[3], a1[NPT], b1[3];
       ld(0, a0, b0);
       __builtin_amdgcn_sched_group_barrier(0x100, NPT + 3, 0);  // pinned order: reads(k+1), MFMAs(k)
 #pragma unroll
@@ -322,7 +324,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int px = (wave * NPT + t) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          if (px < P) sD[px * COUT + ct * 32 + l32] = (__bf16)acc[t][ct][i];
+          if (px < P) sD[px * COUT + ct * 32 + l32] = (E)acc[t][ct][i];
         }
     __syncthreads();
     if (gact) {
@@ -337,11 +339,11 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
       for (int i = 0; i < NCH; ++i) {
         const int px = pg + PG * i;
         if (px < P) {
-          const bf16x8 a8 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(&sD[px * COUT + c8 * 8]));
-          const bf16x8 r8 = __builtin_bit_cast(bf16x8, ad[i]);
-          bf16x8 s8;
+          const E8 a8 = __builtin_bit_cast(E8, *reinterpret_cast<const u32x4*>(&sD[px * COUT + c8 * 8]));
+          const E8 r8 = __builtin_bit_cast(E8, ad[i]);
+          E8 s8;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) s8[j] = (__bf16)((float)a8[j] + (float)r8[j]);
+          for (int j = 0; j < 8; ++j) s8[j] = (E)((float)a8[j] + (float)r8[j]);
           *reinterpret_cast<u32x4*>(&p.dx[((size_t)n * P + px) * COUT + c8 * 8]) = __builtin_bit_cast(u32x4, s8);
         }
       }
@@ -356,9 +358,10 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
 }
 
 // ------------------------------------------------------------------------------------
+template <typename E>
 struct WgradParams {
-  const __bf16* dy;
-  const __bf16* x;
+  const E* dy;
+  const E* x;
   float* part;  // [G][9][96][CIN]
   int N, H, W, G;
 };
@@ -373,8 +376,9 @@ __host__ __device__ inline int wgrad_lds(int H, int W) {
 // PF (16x16 boards, 96 channels): the next sample's dy and x slice are loaded into
 // registers (12 + 4 16-B chunks per thread) while this sample's MFMAs run, and written
 // to LDS after the trailing barrier, so the load round trip leaves the critical path.
-template <int CIN, int T0, int NT, bool PF>
-__device__ __forceinline__ void wgrad_body(const WgradParams& p, __bf16* sDY, __bf16* sX, int gid, int ci0) {
+template <typename E, int CIN, int T0, int NT, bool PF>
+__device__ __forceinline__ void wgrad_body(const WgradParams<E>& p, E* sDY, E* sX, int gid, int ci0) {
+  typedef typename EV<E>::v8 E8;
   constexpr int TAP0 = T0 / 3, TAP1 = (T0 + NT - 1) / 3, NTAP = TAP1 - TAP0 + 1;
   constexpr int XC = CIN < 32 ? CIN : 32;  // real channels of the slice (the stem's 16 + 16 zero)
   constexpr int XCH = XC / 8;
@@ -440,10 +444,10 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, __bf16* sDY, __
     if (PF) {
       // 16 pixel steps, operands double-buffered: step k+1's LDS reads are issued
       // before step k's MFMAs
-      auto ld = [&](int k0, bf16x8 (&a)[3], bf16x8 (&b)[NTAP]) {
+      auto ld = [&](int k0, E8 (&a)[3], E8 (&b)[NTAP]) {
 #pragma unroll
         for (int cot = 0; cot < 3; ++cot) {
-          const __bf16* base = sDY + (k0 + rowoff) * COUT + cot * 32 + col;
+          const E* base = sDY + (k0 + rowoff) * COUT + cot * 32 + col;
           a[cot] = cat8(lds_tr4(base), lds_tr4(base + 4 * COUT));
         }
         const int px0 = k0 + rowoff, px1 = px0 + 4;
@@ -452,14 +456,14 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, __bf16* sDY, __
         for (int j = 0; j < NTAP; ++j)
           b[j] = cat8(lds_tr4(sX + h0 * 32 + tapoff[j] + col), lds_tr4(sX + h1 * 32 + tapoff[j] + col));
       };
-      auto mm = [&](const bf16x8 (&a)[3], const bf16x8 (&b)[NTAP]) {
+      auto mm = [&](const E8 (&a)[3], const E8 (&b)[NTAP]) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           const int tt = T0 + t;
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[tt % 3], b[tt / 3 - TAP0], acc[t], 0, 0, 0);
+          acc[t] = mfma32(a[tt % 3], b[tt / 3 - TAP0], acc[t]);
         }
       };
-      bf16x8 a0[3], b0[NTAP], a1[3], b1[NTAP];
+      E8 a0[3], b0[NTAP], a1[3], b1[NTAP];
       ld(0, a0, b0);
 #pragma unroll
       for (int k0 = 0; k0 < 256; k0 += 32) {
@@ -470,10 +474,10 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, __bf16* sDY, __
       }
     } else
     for (int k0 = 0; k0 < Ppad; k0 += 16) {
-      bf16x8 a[3];
+      E8 a[3];
 #pragma unroll
       for (int cot = 0; cot < 3; ++cot) {
-        const __bf16* base = sDY + (k0 + rowoff) * COUT + cot * 32 + col;
+        const E* base = sDY + (k0 + rowoff) * COUT + cot * 32 + col;
         a[cot] = cat8(lds_tr4(base), lds_tr4(base + 4 * COUT));
       }
       int h[2];
@@ -483,14 +487,14 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, __bf16* sDY, __
         const int r = (int)(((float)px + 0.5f) * invW);
         h[s] = px < P ? (r + 1) * WP + (px - r * W) + 1 : W + 3;  // beyond P: dy rows are 0
       }
-      bf16x8 b[NTAP];
+      E8 b[NTAP];
 #pragma unroll
       for (int j = 0; j < NTAP; ++j)
         b[j] = cat8(lds_tr4(sX + h[0] * 32 + tapoff[j] + col), lds_tr4(sX + h[1] * 32 + tapoff[j] + col));
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int tt = T0 + t;
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[tt % 3], b[tt / 3 - TAP0], acc[t], 0, 0, 0);
+        acc[t] = mfma32(a[tt % 3], b[tt / 3 - TAP0], acc[t]);
       }
     }
     __syncthreads();
@@ -509,13 +513,13 @@ __device__ __forceinline__ void wgrad_body(const WgradParams& p, __bf16* sDY, __
   }
 }
 
-template <int CIN, bool PF>
-__global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams p) {
+template <typename E, int CIN, bool PF>
+__global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams<E> p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NCI = CIN / 32 > 0 ? CIN / 32 : 1;
   const int P = p.H * p.W, Ppad = (P + 15) & ~15;
-  __bf16* sDY = reinterpret_cast<__bf16*>(smem);  // [Ppad][96], rows >= P zero
-  __bf16* sX = sDY + Ppad * COUT;                  // [(H+2)(W+2)][32] zero-halo ci slice
+  E* sDY = reinterpret_cast<E*>(smem);  // [Ppad][96], rows >= P zero
+  E* sX = sDY + Ppad * COUT;                  // [(H+2)(W+2)][32] zero-halo ci slice
   const int tid = threadIdx.x;
   for (int i = P * NC8 + tid; i < Ppad * NC8; i += 256) *reinterpret_cast<u32x4*>(&sDY[i * 8]) = u32x4{0u, 0u, 0u, 0u};
   for (int i = tid; i < (p.H + 2) * (p.W + 2) * 4; i += 256) *reinterpret_cast<u32x4*>(&sX[i * 8]) = u32x4{0u, 0u, 0u, 0u};
@@ -525,10 +529,10 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams p) {
   const int cig = j % NCI, gid = (j / NCI) * 8 + xcd;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   switch (wave) {
-    case 0: wgrad_body<CIN, 0, 7, PF>(p, sDY, sX, gid, cig * 32); break;
-    case 1: wgrad_body<CIN, 7, 7, PF>(p, sDY, sX, gid, cig * 32); break;
-    case 2: wgrad_body<CIN, 14, 7, PF>(p, sDY, sX, gid, cig * 32); break;
-    default: wgrad_body<CIN, 21, 6, PF>(p, sDY, sX, gid, cig * 32); break;
+    case 0: wgrad_body<E, CIN, 0, 7, PF>(p, sDY, sX, gid, cig * 32); break;
+    case 1: wgrad_body<E, CIN, 7, 7, PF>(p, sDY, sX, gid, cig * 32); break;
+    case 2: wgrad_body<E, CIN, 14, 7, PF>(p, sDY, sX, gid, cig * 32); break;
+    default: wgrad_body<E, CIN, 21, 6, PF>(p, sDY, sX, gid, cig * 32); break;
   }
 }
 
@@ -595,34 +599,34 @@ void set_lds_attr(K kernel) {
   (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
-template <int NPT, bool DGRAD, int NCH, bool RM>
-void launch_bwd_data_t(const BwdDataParams& p, int grid, size_t lds, hipStream_t s) {
+template <typename E, int NPT, bool DGRAD, int NCH, bool RM>
+void launch_bwd_data_t(const BwdDataParams<E>& p, int grid, size_t lds, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    set_lds_attr(k_bwd_data<NPT, DGRAD, NCH, RM>);
+    set_lds_attr(k_bwd_data<E, NPT, DGRAD, NCH, RM>);
     attr = true;
   }
-  hipLaunchKernelGGL((k_bwd_data<NPT, DGRAD, NCH, RM>), dim3(grid), dim3(256), lds, s, p);
+  hipLaunchKernelGGL((k_bwd_data<E, NPT, DGRAD, NCH, RM>), dim3(grid), dim3(256), lds, s, p);
 }
 
-template <int NPT, bool DGRAD, int NCH>
-void launch_bwd_data(const BwdDataParams& p, int grid, size_t lds, hipStream_t s) {
-  if (p.rmask) launch_bwd_data_t<NPT, DGRAD, NCH, true>(p, grid, lds, s);
-  else launch_bwd_data_t<NPT, DGRAD, NCH, false>(p, grid, lds, s);
+template <typename E, int NPT, bool DGRAD, int NCH>
+void launch_bwd_data(const BwdDataParams<E>& p, int grid, size_t lds, hipStream_t s) {
+  if (p.rmask) launch_bwd_data_t<E, NPT, DGRAD, NCH, true>(p, grid, lds, s);
+  else launch_bwd_data_t<E, NPT, DGRAD, NCH, false>(p, grid, lds, s);
 }
 
-template <bool DGRAD>
-int dispatch_bwd_data(const BwdDataParams& p, int grid, hipStream_t s) {
+template <typename E, bool DGRAD>
+int dispatch_bwd_data(const BwdDataParams<E>& p, int grid, hipStream_t s) {
   const int P = p.H * p.W;
   const size_t lds = (size_t)bwd_data_lds(P);
   if (lds > 160 * 1024) {
     snprintf(g_err, sizeof g_err, "mc_conv_gn_bwd: board %dx%d needs %zu B LDS", p.H, p.W, lds);
     return MS_EINVAL;
   }
-  if (P <= 128) launch_bwd_data<1, DGRAD, 13>(p, grid, lds, s);
-  else if (P <= 256) launch_bwd_data<2, DGRAD, 13>(p, grid, lds, s);
-  else if (P <= 384) launch_bwd_data<3, DGRAD, 25>(p, grid, lds, s);
-  else if (P <= 512) launch_bwd_data<4, DGRAD, 25>(p, grid, lds, s);
+  if (P <= 128) launch_bwd_data<E, 1, DGRAD, 13>(p, grid, lds, s);
+  else if (P <= 256) launch_bwd_data<E, 2, DGRAD, 13>(p, grid, lds, s);
+  else if (P <= 384) launch_bwd_data<E, 3, DGRAD, 25>(p, grid, lds, s);
+  else if (P <= 512) launch_bwd_data<E, 4, DGRAD, 25>(p, grid, lds, s);
   else {
     snprintf(g_err, sizeof g_err, "mc_conv_gn_bwd: %d pixels > 512 unsupported", P);
     return MS_EINVAL;
@@ -630,23 +634,23 @@ int dispatch_bwd_data(const BwdDataParams& p, int grid, hipStream_t s) {
   return MS_OK;
 }
 
-template <int CIN, bool PF>
-void launch_wgrad_t(const WgradParams& p, int grid, size_t lds, hipStream_t s) {
+template <typename E, int CIN, bool PF>
+void launch_wgrad_t(const WgradParams<E>& p, int grid, size_t lds, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    set_lds_attr(k_wgrad<CIN, PF>);
+    set_lds_attr(k_wgrad<E, CIN, PF>);
     attr = true;
   }
-  hipLaunchKernelGGL((k_wgrad<CIN, PF>), dim3(grid), dim3(256), lds, s, p);
+  hipLaunchKernelGGL((k_wgrad<E, CIN, PF>), dim3(grid), dim3(256), lds, s, p);
 }
 
-template <int CIN>
-void launch_wgrad(const WgradParams& p, int grid, size_t lds, hipStream_t s) {
+template <typename E, int CIN>
+void launch_wgrad(const WgradParams<E>& p, int grid, size_t lds, hipStream_t s) {
   // 16x16 boards with 96 channels: the register prefetch of the next sample's dy and x slice
   if constexpr (CIN == 96) {
-    if (p.H == 16 && p.W == 16) return launch_wgrad_t<CIN, true>(p, grid, lds, s);
+    if (p.H == 16 && p.W == 16) return launch_wgrad_t<E, CIN, true>(p, grid, lds, s);
   }
-  launch_wgrad_t<CIN, false>(p, grid, lds, s);
+  launch_wgrad_t<E, CIN, false>(p, grid, lds, s);
 }
 
 int check_launch(const char* what) {
@@ -656,6 +660,52 @@ int check_launch(const char* what) {
     return MS_EHIP;
   }
   return MS_OK;
+}
+
+template <typename E>
+int run_bwd(const uint16_t* dout, const uint16_t* out, const uint8_t* relu_mask, const uint16_t* ysave,
+            const float* stats, const float* gamma, const float* dmask, const uint16_t* x, const uint16_t* wT,
+            const uint16_t* addend, uint16_t* dy, uint16_t* dz, uint16_t* dx, float* dw, float* dgn, float* work,
+            int32_t n, int32_t h, int32_t w_, int32_t cin, hipStream_t s) {
+  const Plan pl = make_plan(n, h, w_, cin);
+  BwdDataParams<E> bp;
+  bp.dout = reinterpret_cast<const E*>(dout);
+  bp.out = reinterpret_cast<const E*>(out);
+  bp.rmask = relu_mask;
+  bp.y = reinterpret_cast<const E*>(ysave);
+  bp.stats = stats;
+  bp.gamma = gamma;
+  bp.dmask = dmask;
+  bp.wT = reinterpret_cast<const E*>(wT);
+  bp.addend = reinterpret_cast<const E*>(addend);
+  bp.dy = reinterpret_cast<E*>(dy);
+  bp.dz = reinterpret_cast<E*>(dz);
+  bp.dx = reinterpret_cast<E*>(dx);
+  bp.part = work;
+  bp.N = n;
+  bp.H = h;
+  bp.W = w_;
+  int rc = wT ? dispatch_bwd_data<E, true>(bp, pl.grid_d, s) : dispatch_bwd_data<E, false>(bp, pl.grid_d, s);
+  if (rc) return rc;
+  if ((rc = check_launch("k_bwd_data"))) return rc;
+  launch_reduce((const float*)work, pl.grid_d, (int64_t)3 * COUT, dgn, s);
+  if ((rc = check_launch("k_reduce"))) return rc;
+
+  WgradParams<E> wp;
+  wp.dy = reinterpret_cast<const E*>(dy);
+  wp.x = reinterpret_cast<const E*>(x);
+  wp.part = work + pl.gn_part;
+  wp.N = n;
+  wp.H = h;
+  wp.W = w_;
+  wp.G = pl.G;
+  const size_t lds = (size_t)wgrad_lds(h, w_);
+  if (cin == 96) launch_wgrad<E, 96>(wp, pl.grid_w, lds, s);
+  else launch_wgrad<E, 16>(wp, pl.grid_w, lds, s);
+  if ((rc = check_launch("k_wgrad"))) return rc;
+  const int64_t nw = (int64_t)9 * COUT * cin;
+  launch_reduce((const float*)(work + pl.gn_part), pl.G, nw, dw, s);
+  return check_launch("k_reduce");
 }
 
 }  // namespace
@@ -673,7 +723,7 @@ int mc_conv_gn_bwd(const uint16_t* dout, const uint16_t* out, const uint8_t* rel
                    const float* gamma, const float* dmask, const uint16_t* x, const uint16_t* wT,
                    const uint16_t* addend, uint16_t* dy, uint16_t* dz, uint16_t* dx, float* dw, float* dgn,
                    float* work, int64_t work_floats, int32_t n, int32_t h, int32_t w_, int32_t cin,
-                   void* stream) {
+                   int32_t dtype, void* stream) {
   if (!dout || (!out && !relu_mask) || !ysave || !stats || !gamma || !x || !dy || !dw || !dgn || !work || n <= 0 || h <= 0 ||
       w_ <= 0) {
     snprintf(g_err, sizeof g_err, "mc_conv_gn_bwd: bad argument");
@@ -698,44 +748,14 @@ int mc_conv_gn_bwd(const uint16_t* dout, const uint16_t* out, const uint8_t* rel
     return MS_EINVAL;
   }
   hipStream_t s = (hipStream_t)stream;
-  BwdDataParams bp;
-  bp.dout = reinterpret_cast<const __bf16*>(dout);
-  bp.out = reinterpret_cast<const __bf16*>(out);
-  bp.rmask = relu_mask;
-  bp.y = reinterpret_cast<const __bf16*>(ysave);
-  bp.stats = stats;
-  bp.gamma = gamma;
-  bp.dmask = dmask;
-  bp.wT = reinterpret_cast<const __bf16*>(wT);
-  bp.addend = reinterpret_cast<const __bf16*>(addend);
-  bp.dy = reinterpret_cast<__bf16*>(dy);
-  bp.dz = reinterpret_cast<__bf16*>(dz);
-  bp.dx = reinterpret_cast<__bf16*>(dx);
-  bp.part = work;
-  bp.N = n;
-  bp.H = h;
-  bp.W = w_;
-  int rc = wT ? dispatch_bwd_data<true>(bp, pl.grid_d, s) : dispatch_bwd_data<false>(bp, pl.grid_d, s);
-  if (rc) return rc;
-  if ((rc = check_launch("k_bwd_data"))) return rc;
-  launch_reduce((const float*)work, pl.grid_d, (int64_t)3 * COUT, dgn, s);
-  if ((rc = check_launch("k_reduce"))) return rc;
-
-  WgradParams wp;
-  wp.dy = reinterpret_cast<const __bf16*>(dy);
-  wp.x = reinterpret_cast<const __bf16*>(x);
-  wp.part = work + pl.gn_part;
-  wp.N = n;
-  wp.H = h;
-  wp.W = w_;
-  wp.G = pl.G;
-  const size_t lds = (size_t)wgrad_lds(h, w_);
-  if (cin == 96) launch_wgrad<96>(wp, pl.grid_w, lds, s);
-  else launch_wgrad<16>(wp, pl.grid_w, lds, s);
-  if ((rc = check_launch("k_wgrad"))) return rc;
-  const int64_t nw = (int64_t)9 * COUT * cin;
-  launch_reduce((const float*)(work + pl.gn_part), pl.G, nw, dw, s);
-  return check_launch("k_reduce");
+  if (dtype == MC_DT_BF16)
+    return run_bwd<__bf16>(dout, out, relu_mask, ysave, stats, gamma, dmask, x, wT, addend, dy, dz, dx, dw, dgn, work, n, h,
+                           w_, cin, s);
+  if (dtype == MC_DT_F16)
+    return run_bwd<_Float16>(dout, out, relu_mask, ysave, stats, gamma, dmask, x, wT, addend, dy, dz, dx, dw, dgn, work, n,
+                             h, w_, cin, s);
+  snprintf(g_err, sizeof g_err, "mc_conv_gn_bwd: dtype %d unsupported (0 bf16, 1 f16)", dtype);
+  return MS_EINVAL;
 }
 
 }  // extern "C"

@@ -10,11 +10,35 @@ namespace mc {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 // native vector: HIP's uint4 struct copies through memcpy and is left in scratch
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// 16-bit activation / weight element: __bf16 (bf16 autocast) or _Float16 (fp16 autocast,
+// the reference's own training precision); all sums are f32 either way
+template <typename E>
+struct EV;
+template <>
+struct EV<__bf16> {
+  typedef bf16x8 v8;
+  typedef bf16x4 v4;
+};
+template <>
+struct EV<_Float16> {
+  typedef f16x8 v8;
+  typedef f16x4 v4;
+};
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 mfma32(f16x8 a, f16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
 
 constexpr int COUT = 96;  // trunk width of the shipped configs (stem_channels)
 constexpr int NGRP = 6;   // GroupNorm groups (96 / 16)
@@ -44,9 +68,10 @@ __device__ __forceinline__ float readlane_f(float v, int l) {
 
 // ds_read_b64_tr_b16: per 16-lane group, lane 4q+p addresses row q / columns
 // 4p..4p+3 of a 4x16 block of 16-bit elements; lane i receives column i.
-__device__ __forceinline__ bf16x4 lds_tr4(const __bf16* p) {
+template <typename E>
+__device__ __forceinline__ typename EV<E>::v4 lds_tr4(const E* p) {
   const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
-  return __builtin_bit_cast(bf16x4, v);
+  return __builtin_bit_cast(typename EV<E>::v4, v);
 }
 
 // An SGPR zero the compiler cannot see through: indexing loop-invariant LDS data with
@@ -69,5 +94,11 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 __device__ __forceinline__ bf16x8 cat8(bf16x4 lo, bf16x4 hi) {
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
+__device__ __forceinline__ f16x8 cat8(f16x4 lo, f16x4 hi) {
+  return f16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// the dtype argument of the mscnn.h entry points
+enum { MC_DT_BF16 = 0, MC_DT_F16 = 1 };
 
 }  // namespace mc

@@ -37,9 +37,10 @@ constexpr int WP = 104;      // padded weight row (elements): conflict-free ds_r
 constexpr int TR = 128;      // rows per tile
 constexpr int PART = NH * C + 2 * NH;  // per-workgroup partial: dW1 | dw2 | db1
 
+template <typename E>
 struct HeadFwdParams {
-  const __bf16* f;
-  const __bf16* w1;  // [nh][96]
+  const E* f;
+  const E* w1;  // [nh][96]
   const float* b1;
   const float* w2;
   const float* b2;
@@ -48,10 +49,11 @@ struct HeadFwdParams {
   int64_t M;
 };
 
-template <bool MINE>
-__global__ __launch_bounds__(256, 2) void k_heads_fwd(HeadFwdParams p) {
+template <typename E, bool MINE>
+__global__ __launch_bounds__(256, 2) void k_heads_fwd(HeadFwdParams<E> p) {
+  typedef typename EV<E>::v8 E8;
   constexpr int NT = MINE ? 6 : 3;
-  __shared__ __attribute__((aligned(16))) __bf16 sW[NT * 32 * WP];
+  __shared__ __attribute__((aligned(16))) E sW[NT * 32 * WP];
   __shared__ __attribute__((aligned(16))) float sB1[NT * 32], sW2[NT * 32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hh = lane >> 5;
   for (int i = tid; i < NT * 32 * 12; i += 256) {
@@ -72,21 +74,21 @@ __global__ __launch_bounds__(256, 2) void k_heads_fwd(HeadFwdParams p) {
     // f rows: unconditional loads from a clamped row (a guarded load sits in its own exec
     // branch); rows past M are computed and not stored
     const int64_t rowc = valid ? row : p.M - 1;
-    bf16x8 b[6];
+    E8 b[6];
 #pragma unroll
     for (int ks = 0; ks < 6; ++ks)
-      b[ks] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(&p.f[rowc * C + ks * 16 + 8 * hh]));
+      b[ks] = __builtin_bit_cast(E8, *reinterpret_cast<const u32x4*>(&p.f[rowc * C + ks * 16 + 8 * hh]));
     f32x16 acc[NT];
 #pragma unroll
     for (int ct = 0; ct < NT; ++ct)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[ct][i] = 0.f;
     // W1 operands double-buffered across k steps, order pinned (reads of k+1, MFMAs of k)
-    bf16x8 A[2][NT];
-    auto ld = [&](int ks, bf16x8 (&a)[NT]) {
+    E8 A[2][NT];
+    auto ld = [&](int ks, E8 (&a)[NT]) {
 #pragma unroll
       for (int ct = 0; ct < NT; ++ct)
-        a[ct] = *reinterpret_cast<const bf16x8*>(&sW[(ct * 32 + l32) * WP + ks * 16 + 8 * hh + zo]);
+        a[ct] = *reinterpret_cast<const E8*>(&sW[(ct * 32 + l32) * WP + ks * 16 + 8 * hh + zo]);
     };
     ld(0, A[0]);
     __builtin_amdgcn_sched_group_barrier(0x020, 6, 0);  // the six f loads first, together
@@ -98,7 +100,7 @@ __global__ __launch_bounds__(256, 2) void k_heads_fwd(HeadFwdParams p) {
         __builtin_amdgcn_sched_group_barrier(0x100, NT, 0);
       }
 #pragma unroll
-      for (int ct = 0; ct < NT; ++ct) acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[ks & 1][ct], b[ks], acc[ct], 0, 0, 0);
+      for (int ct = 0; ct < NT; ++ct) acc[ct] = mfma32(A[ks & 1][ct], b[ks], acc[ct]);
       __builtin_amdgcn_sched_group_barrier(0x008, NT, 0);
     }
     // acc[ct][r] = H^T[c = ct*32 + 8*(r>>2) + 4*hh + (r&3)][px = l32]
@@ -123,16 +125,17 @@ __global__ __launch_bounds__(256, 2) void k_heads_fwd(HeadFwdParams p) {
 }
 
 // ------------------------------------------------------------------------------------
+template <typename E>
 struct HeadBwdParams {
-  const __bf16* f;
+  const E* f;
   const float* dlp;
   const float* dlm;
-  const __bf16* w1;   // [192][96]
-  const __bf16* w1pT; // [96 k][96 c] policy W1 transposed
+  const E* w1;   // [192][96]
+  const E* w1pT; // [96 k][96 c] policy W1 transposed
   const float* b1;
   const float* w2;
   const float* gadd;  // [M / P][96] or null: added to df (the value head's pooled gradient / P)
-  __bf16* df;
+  E* df;
   float* part;        // [gridDim][PART]
   int64_t M;
   int P;
@@ -147,19 +150,22 @@ __device__ __forceinline__ int sd_off(int r, int col) {
   return r * NH + 8 * ((col >> 3) ^ ((((r >> 1) & 1) << 2) | ((r >> 2) & 3))) + (col & 7);
 }
 
+template <typename E>
 struct HeadLds {
-  __bf16 w[NH * WP];     // W1 rows [c][k]
-  __bf16 wt[C * WP];     // policy W1^T rows [k][c]
-  __bf16 f[TR * C];      // swizzled f tile
-  __bf16 dh[TR * NH];    // swizzled dh image
-  __bf16 df[TR * C];     // df rows, each wave's 32 rows staged for contiguous 16-B stores
+  E w[NH * WP];     // W1 rows [c][k]
+  E wt[C * WP];     // policy W1^T rows [k][c]
+  E f[TR * C];      // swizzled f tile
+  E dh[TR * NH];    // swizzled dh image
+  E df[TR * C];     // df rows, each wave's 32 rows staged for contiguous 16-B stores
   float dl[2][TR];
   float b1[NH], w2[NH];
   float red[2][NH];
 };
 
-template <int T0, int NTW>
-__device__ __forceinline__ void heads_bwd_body(const HeadBwdParams& p, HeadLds& L) {
+template <typename E, int T0, int NTW>
+__device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLds<E>& L) {
+  typedef typename EV<E>::v8 E8;
+  typedef typename EV<E>::v4 E4;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hh = lane >> 5;
   const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
   f32x16 dwacc[NTW];
@@ -215,11 +221,11 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams& p, HeadLds& 
       const int ra = wave * 32 + l32 + zo;
 #pragma unroll
       for (int ks = 0; ks < 6; ++ks) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&L.f[sf_off(ra, ks * 16 + 8 * hh)]);
+        const E8 a = *reinterpret_cast<const E8*>(&L.f[sf_off(ra, ks * 16 + 8 * hh)]);
 #pragma unroll
         for (int ct = 0; ct < 6; ++ct) {
-          const bf16x8 b = *reinterpret_cast<const bf16x8*>(&L.w[(ct * 32 + l32) * WP + ks * 16 + 8 * hh + zo]);
-          acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[ct], 0, 0, 0);
+          const E8 b = *reinterpret_cast<const E8*>(&L.w[(ct * 32 + l32) * WP + ks * 16 + 8 * hh + zo]);
+          acc[ct] = mfma32(a, b, acc[ct]);
         }
       }
       // acc[ct][r] = H[px = wave*32 + 8*(r>>2) + 4*hh + (r&3)][c = ct*32 + l32]
@@ -235,7 +241,7 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams& p, HeadLds& 
           dw2acc[ct] += hv * dl;
           const float dh = hv > 0.f ? dl * w2c : 0.f;
           db1acc[ct] += dh;
-          L.dh[sd_off(pr, c)] = (__bf16)dh;
+          L.dh[sd_off(pr, c)] = (E)dh;
         }
       }
     }
@@ -266,11 +272,11 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams& p, HeadLds& 
       }
 #pragma unroll
       for (int ks = 0; ks < 6; ++ks) {
-        const bf16x8 b = *reinterpret_cast<const bf16x8*>(&L.dh[sd_off(rb, ks * 16 + 8 * hh)]);
+        const E8 b = *reinterpret_cast<const E8*>(&L.dh[sd_off(rb, ks * 16 + 8 * hh)]);
 #pragma unroll
         for (int kt = 0; kt < 3; ++kt) {
-          const bf16x8 a = *reinterpret_cast<const bf16x8*>(&L.wt[(kt * 32 + l32) * WP + ks * 16 + 8 * hh + zo]);
-          acc2[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc2[kt], 0, 0, 0);
+          const E8 a = *reinterpret_cast<const E8*>(&L.wt[(kt * 32 + l32) * WP + ks * 16 + 8 * hh + zo]);
+          acc2[kt] = mfma32(a, b, acc2[kt]);
         }
       }
       // acc2[kt][r] = df[px = wave*32 + l32][k = kt*32 + 8*(r>>2) + 4*hh + (r&3)]:
@@ -284,8 +290,8 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams& p, HeadLds& 
           float v[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[j] = acc2[kt][4 * gg + j];
-          *reinterpret_cast<bf16x4*>(&L.df[rb * C + k0]) =
-              bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+          *reinterpret_cast<E4*>(&L.df[rb * C + k0]) =
+              E4{(E)v[0], (E)v[1], (E)v[2], (E)v[3]};
         }
       // (LDS operations of one wave complete in order: its own rows read back below)
       const int lane64 = tid & 63;
@@ -301,7 +307,7 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams& p, HeadLds& 
 #pragma unroll 2
     for (int kk = 0; kk < TR / 16; ++kk) {
       const int r0 = kk * 16 + 8 * (g >> 1) + q + zo;
-      bf16x8 av[6], bv[3];
+      E8 av[6], bv[3];
 #pragma unroll
       for (int ct = T0 / 3; ct <= (T0 + NTW - 1) / 3; ++ct) {
         const int col = ct * 32 + 16 * (g & 1) + 4 * pp;
@@ -315,7 +321,7 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams& p, HeadLds& 
 #pragma unroll
       for (int t = 0; t < NTW; ++t) {
         const int tt = T0 + t;
-        dwacc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[tt / 3], bv[tt % 3], dwacc[t], 0, 0, 0);
+        dwacc[t] = mfma32(av[tt / 3], bv[tt % 3], dwacc[t]);
       }
     }
     __syncthreads();  // f / dh images are re-staged by the next tile
@@ -338,9 +344,10 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams& p, HeadLds& 
   }
 }
 
-__global__ __launch_bounds__(256, 1) void k_heads_bwd(HeadBwdParams p) {
+template <typename E>
+__global__ __launch_bounds__(256, 1) void k_heads_bwd(HeadBwdParams<E> p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  HeadLds& L = *reinterpret_cast<HeadLds*>(smem);
+  HeadLds<E>& L = *reinterpret_cast<HeadLds<E>*>(smem);
   const int tid = threadIdx.x;
   for (int i = tid; i < NH * 12; i += 256) {
     const int c = i / 12, k8 = i - c * 12;
@@ -358,10 +365,10 @@ __global__ __launch_bounds__(256, 1) void k_heads_bwd(HeadBwdParams p) {
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   switch (wave) {  // 18 dW1 tiles (6 c-tiles x 3 k-tiles) split 5/5/4/4
-    case 0: heads_bwd_body<0, 5>(p, L); break;
-    case 1: heads_bwd_body<5, 5>(p, L); break;
-    case 2: heads_bwd_body<10, 4>(p, L); break;
-    default: heads_bwd_body<14, 4>(p, L); break;
+    case 0: heads_bwd_body<E, 0, 5>(p, L); break;
+    case 1: heads_bwd_body<E, 5, 5>(p, L); break;
+    case 2: heads_bwd_body<E, 10, 4>(p, L); break;
+    default: heads_bwd_body<E, 14, 4>(p, L); break;
   }
   __syncthreads();
   float* part = p.part + (size_t)blockIdx.x * PART;
@@ -397,19 +404,12 @@ int check(const char* what) {
   return MS_OK;
 }
 
-}  // namespace
-
-extern "C" {
-
-int mc_heads_fwd(const uint16_t* f, const uint16_t* w1, const float* b1, const float* w2, const float* b2,
-                 float* out_p, float* out_m, int64_t M, void* stream) {
-  if (!f || !w1 || !b1 || !w2 || !b2 || !out_p || M <= 0) {
-    snprintf(g_err, sizeof g_err, "mc_heads_fwd: bad argument");
-    return MS_EINVAL;
-  }
-  HeadFwdParams p;
-  p.f = reinterpret_cast<const __bf16*>(f);
-  p.w1 = reinterpret_cast<const __bf16*>(w1);
+template <typename E>
+int run_heads_fwd(const uint16_t* f, const uint16_t* w1, const float* b1, const float* w2, const float* b2,
+                  float* out_p, float* out_m, int64_t M, hipStream_t s) {
+  HeadFwdParams<E> p;
+  p.f = reinterpret_cast<const E*>(f);
+  p.w1 = reinterpret_cast<const E*>(w1);
   p.b1 = b1;
   p.w2 = w2;
   p.b2 = b2;
@@ -419,10 +419,56 @@ int mc_heads_fwd(const uint16_t* f, const uint16_t* w1, const float* b1, const f
   const int64_t ntiles = (M + TR - 1) / TR;
   const int cap = 2 * num_cus();
   const int grid = (int)(ntiles < cap ? ntiles : cap);
-  hipStream_t s = (hipStream_t)stream;
-  if (out_m) hipLaunchKernelGGL(k_heads_fwd<true>, dim3(grid), dim3(256), 0, s, p);
-  else hipLaunchKernelGGL(k_heads_fwd<false>, dim3(grid), dim3(256), 0, s, p);
+  if (out_m) hipLaunchKernelGGL((k_heads_fwd<E, true>), dim3(grid), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((k_heads_fwd<E, false>), dim3(grid), dim3(256), 0, s, p);
   return check("k_heads_fwd");
+}
+
+template <typename E>
+int run_heads_bwd(const uint16_t* f, const float* dlp, const float* dlm, const uint16_t* w1, const uint16_t* w1pT,
+                  const float* b1, const float* w2, const float* gadd, int32_t P, uint16_t* df, float* dw1, float* db1,
+                  float* dw2, float* work, int64_t M, int grid, hipStream_t s) {
+  HeadBwdParams<E> p;
+  p.f = reinterpret_cast<const E*>(f);
+  p.dlp = dlp;
+  p.dlm = dlm;
+  p.w1 = reinterpret_cast<const E*>(w1);
+  p.w1pT = reinterpret_cast<const E*>(w1pT);
+  p.b1 = b1;
+  p.w2 = w2;
+  p.gadd = gadd;
+  p.df = reinterpret_cast<E*>(df);
+  p.part = work;
+  p.M = M;
+  p.P = P;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_heads_bwd<E>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_heads_bwd<E>, dim3(grid), dim3(256), sizeof(HeadLds<E>), s, p);
+  int rc = check("k_heads_bwd");
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_heads_reduce, dim3((PART + 255) / 256), dim3(256), 0, s, (const float*)work, grid, dw1, dw2,
+                     db1);
+  return check("k_heads_reduce");
+}
+
+}  // namespace
+
+extern "C" {
+
+int mc_heads_fwd(const uint16_t* f, const uint16_t* w1, const float* b1, const float* w2, const float* b2,
+                 float* out_p, float* out_m, int64_t M, int32_t dtype, void* stream) {
+  if (!f || !w1 || !b1 || !w2 || !b2 || !out_p || M <= 0) {
+    snprintf(g_err, sizeof g_err, "mc_heads_fwd: bad argument");
+    return MS_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MC_DT_BF16) return run_heads_fwd<__bf16>(f, w1, b1, w2, b2, out_p, out_m, M, s);
+  if (dtype == MC_DT_F16) return run_heads_fwd<_Float16>(f, w1, b1, w2, b2, out_p, out_m, M, s);
+  snprintf(g_err, sizeof g_err, "mc_heads_fwd: dtype %d unsupported (0 bf16, 1 f16)", dtype);
+  return MS_EINVAL;
 }
 
 int64_t mc_heads_bwd_workspace(int64_t M) {
@@ -432,7 +478,7 @@ int64_t mc_heads_bwd_workspace(int64_t M) {
 
 int mc_heads_bwd(const uint16_t* f, const float* dlp, const float* dlm, const uint16_t* w1, const uint16_t* w1pT,
                  const float* b1, const float* w2, const float* gadd, int32_t P, uint16_t* df, float* dw1,
-                 float* db1, float* dw2, float* work, int64_t work_floats, int64_t M, void* stream) {
+                 float* db1, float* dw2, float* work, int64_t work_floats, int64_t M, int32_t dtype, void* stream) {
   if (!f || !dlp || !w1 || !w1pT || !b1 || !w2 || !df || !dw1 || !db1 || !dw2 || !work || M <= 0 ||
       (gadd && P <= 0)) {
     snprintf(g_err, sizeof g_err, "mc_heads_bwd: bad argument");
@@ -443,31 +489,12 @@ int mc_heads_bwd(const uint16_t* f, const float* dlp, const float* dlm, const ui
     snprintf(g_err, sizeof g_err, "mc_heads_bwd: workspace too small");
     return MS_EINVAL;
   }
-  HeadBwdParams p;
-  p.f = reinterpret_cast<const __bf16*>(f);
-  p.dlp = dlp;
-  p.dlm = dlm;
-  p.w1 = reinterpret_cast<const __bf16*>(w1);
-  p.w1pT = reinterpret_cast<const __bf16*>(w1pT);
-  p.b1 = b1;
-  p.w2 = w2;
-  p.gadd = gadd;
-  p.df = reinterpret_cast<__bf16*>(df);
-  p.part = work;
-  p.M = M;
-  p.P = P;
   hipStream_t s = (hipStream_t)stream;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_heads_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
-  hipLaunchKernelGGL(k_heads_bwd, dim3(grid), dim3(256), sizeof(HeadLds), s, p);
-  int rc = check("k_heads_bwd");
-  if (rc) return rc;
-  hipLaunchKernelGGL(k_heads_reduce, dim3((PART + 255) / 256), dim3(256), 0, s, (const float*)work, grid, dw1, dw2,
-                     db1);
-  return check("k_heads_reduce");
+  if (dtype == MC_DT_BF16) return run_heads_bwd<__bf16>(f, dlp, dlm, w1, w1pT, b1, w2, gadd, P, df, dw1, db1, dw2, work, M, grid, s);
+  if (dtype == MC_DT_F16)
+    return run_heads_bwd<_Float16>(f, dlp, dlm, w1, w1pT, b1, w2, gadd, P, df, dw1, db1, dw2, work, M, grid, s);
+  snprintf(g_err, sizeof g_err, "mc_heads_bwd: dtype %d unsupported (0 bf16, 1 f16)", dtype);
+  return MS_EINVAL;
 }
 
 }  // extern "C"

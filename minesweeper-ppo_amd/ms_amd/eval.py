@@ -209,7 +209,7 @@ def main(argv=None) -> None:
     ap.add_argument("--progress", action="store_true")
     ap.add_argument("--reveal_only", action="store_true")
     ap.add_argument("--debug_eval", action="store_true", help="accepted; not implemented on device")
-    ap.add_argument("--amp", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--amp", choices=["fp32", "bf16", "fp16"], default="fp32")
     args = ap.parse_args(argv)
     device = torch.device("cuda")
     if args.ckpt:
@@ -242,7 +242,7 @@ def main(argv=None) -> None:
                            num_envs=min(args.num_envs, args.episodes),
                            progress_every=(max(1, args.episodes // 4) if args.progress else 0),
                            reveal_only=args.reveal_only,
-                           amp_dtype=torch.bfloat16 if args.amp == "bf16" else None)
+                           amp_dtype={"bf16": torch.bfloat16, "fp16": torch.float16}.get(args.amp))
     summary = {"checkpoint": os.path.basename(ckpt), "model": name, **metrics}
     for k, v in summary.items():
         print(f"{k}: {v:.3f}" if isinstance(v, float) and np.isfinite(v) else f"{k}: {v}")

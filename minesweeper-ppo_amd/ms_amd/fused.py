@@ -1,7 +1,8 @@
 """Fused MFMA residual-CNN layer ops (csrc/mscnn.hip, C ABI include/mscnn.h).
 
-Activations are NHWC bf16 [N, H*W, C]; weights are re-laid out per call as
-bf16 [9, 96, CIN] (tap-major). These ops replace, for CNNResidualPolicy
+Activations are NHWC [N, H*W, C] in a 16-bit type: bf16 (bf16 autocast) or fp16 (fp16
+autocast, the reference's training precision, ppo.py:25); weights are re-laid out as
+[9, 96, CIN] (tap-major) of the same type. These ops replace, for CNNResidualPolicy
 (minesweeper/models/cnn_residual.py:7-96), the chain conv3x3 -> GroupNorm ->
 [+residual] -> ReLU -> [Dropout2d] with one kernel per layer.
 """
@@ -17,6 +18,13 @@ from . import _lib as L
 
 COUT = 96
 NGROUPS = 6
+DTYPES = {torch.bfloat16: 0, torch.float16: 1}  # MC_DTYPE_BF16 / MC_DTYPE_F16 (include/mscnn.h)
+
+
+def _dt(t: torch.Tensor) -> int:
+    if t.dtype not in DTYPES:
+        raise TypeError(f"fused kernels take bf16 or fp16 activations, got {t.dtype}")
+    return DTYPES[t.dtype]
 
 
 def _fn(name, argtypes):
@@ -38,22 +46,22 @@ def _check(rc):
         raise L.MsEnvError(lib.mc_last_error().decode(errors="replace"))
 
 
-def prep_weight(w: torch.Tensor, cin_pad: int) -> torch.Tensor:
-    """[96, cin, 3, 3] (f32 nn.Conv2d weight) -> bf16 [9, 96, cin_pad], tap = 3*ky + kx."""
+def prep_weight(w: torch.Tensor, cin_pad: int, dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
+    """[96, cin, 3, 3] (f32 nn.Conv2d weight) -> ``dtype`` [9, 96, cin_pad], tap = 3*ky + kx."""
     co, ci = w.shape[0], w.shape[1]
     wt = w.permute(2, 3, 0, 1).reshape(9, co, ci)
     if cin_pad > ci:
         wt = torch.nn.functional.pad(wt, (0, cin_pad - ci))
-    return wt.to(torch.bfloat16).contiguous()
+    return wt.to(dtype).contiguous()
 
 
-def obs_to_nhwc(obs: torch.Tensor, cin_pad: int = 16) -> torch.Tensor:
-    """f32 [N, 10, H, W] one-hot observation -> bf16 [N, H*W, cin_pad] (exact: values are 0/1)."""
+def obs_to_nhwc(obs: torch.Tensor, cin_pad: int = 16, dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
+    """f32 [N, 10, H, W] one-hot observation -> ``dtype`` [N, H*W, cin_pad] (exact: values are 0/1)."""
     n, c, h, w = obs.shape
     x = obs.permute(0, 2, 3, 1).reshape(n, h * w, c)
     if cin_pad > c:
         x = torch.nn.functional.pad(x, (0, cin_pad - c))
-    return x.to(torch.bfloat16).contiguous()
+    return x.to(dtype).contiguous()
 
 
 def conv_gn_fwd(x: torch.Tensor, wt: torch.Tensor, bias: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor,
@@ -63,24 +71,25 @@ def conv_gn_fwd(x: torch.Tensor, wt: torch.Tensor, bias: torch.Tensor, gamma: to
     plus the ReLU bitmask (u8 [N, P, 12], bit j of byte c8 = out[..., 8*c8 + j] > 0) with want_mask."""
     global _fwd
     if _fwd is None:
-        _fwd = _fn("mc_conv_gn_fwd", [_vp] * 11 + [_i32] * 4 + [_f32, _vp])
+        _fwd = _fn("mc_conv_gn_fwd", [_vp] * 11 + [_i32] * 4 + [_f32, _i32, _vp])
     n, p, cin = x.shape
-    assert p == H * W and x.dtype == torch.bfloat16 and x.is_contiguous()
-    assert wt.shape == (9, COUT, cin) and wt.dtype == torch.bfloat16 and wt.is_contiguous()
+    dt = _dt(x)
+    assert p == H * W and x.is_contiguous()
+    assert wt.shape == (9, COUT, cin) and wt.dtype == x.dtype and wt.is_contiguous()
     dev = x.device
-    out = torch.empty((n, p, COUT), dtype=torch.bfloat16, device=dev)
+    out = torch.empty((n, p, COUT), dtype=x.dtype, device=dev)
     y = torch.empty_like(out) if save else None
     stats = torch.empty((n, NGROUPS, 2), dtype=torch.float32, device=dev) if save else None
     rmask = torch.empty((n, p, COUT // 8), dtype=torch.uint8, device=dev) if want_mask else None
     if res is not None:
-        assert res.shape == out.shape and res.dtype == torch.bfloat16 and res.is_contiguous()
+        assert res.shape == out.shape and res.dtype == x.dtype and res.is_contiguous()
     if dmask is not None:
         dmask = dmask.to(torch.float32).contiguous()
         assert dmask.shape == (n, COUT)
     f32c = lambda t: t.detach().to(torch.float32).contiguous()  # noqa: E731
     b, g, be = f32c(bias), f32c(gamma), f32c(beta)
     _check(_fwd(L.ptr(x), L.ptr(wt), L.ptr(b), L.ptr(g), L.ptr(be), L.ptr(res), L.ptr(dmask), L.ptr(out),
-                L.ptr(y), L.ptr(stats), L.ptr(rmask), n, H, W, cin, eps, L.stream_ptr(dev)))
+                L.ptr(y), L.ptr(stats), L.ptr(rmask), n, H, W, cin, eps, dt, L.stream_ptr(dev)))
     return (out, y, stats, rmask) if want_mask else (out, y, stats)
 
 
@@ -88,10 +97,10 @@ _bwd = None
 _bwd_ws = None
 
 
-def prep_weight_t(w: torch.Tensor) -> torch.Tensor:
-    """[96, 96, 3, 3] nn.Conv2d weight -> bf16 [9, ci, co] (the dgrad operand W[tap]^T)."""
+def prep_weight_t(w: torch.Tensor, dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
+    """[96, 96, 3, 3] nn.Conv2d weight -> ``dtype`` [9, ci, co] (the dgrad operand W[tap]^T)."""
     co, ci = w.shape[0], w.shape[1]
-    return w.detach().permute(2, 3, 1, 0).reshape(9, ci, co).to(torch.bfloat16).contiguous()
+    return w.detach().permute(2, 3, 1, 0).reshape(9, ci, co).to(dtype).contiguous()
 
 
 def dw_to_conv(dw: torch.Tensor, cin_real: int) -> torch.Tensor:
@@ -104,32 +113,33 @@ def conv_gn_bwd(dout: torch.Tensor, out: Optional[torch.Tensor], y: torch.Tensor
                 dmask: Optional[torch.Tensor] = None, addend: Optional[torch.Tensor] = None, want_dz: bool = False,
                 rmask: Optional[torch.Tensor] = None):
     """Backward of conv_gn_fwd. Returns (dx | None, dz | None, dw f32 [9,96,cin], dgn f32 [3,96] =
-    d gamma, d beta, d bias). dx (bf16, NHWC) is produced iff the dgrad weights ``wT`` are given.
+    d gamma, d beta, d bias). dx (x's 16-bit type, NHWC) is produced iff the dgrad weights ``wT`` are given.
     ``rmask`` (the forward's ReLU bitmask) replaces the sign test on ``out``; one of them is needed."""
     global _bwd, _bwd_ws
     if _bwd is None:
-        _bwd = _fn("mc_conv_gn_bwd", [_vp] * 16 + [ctypes.c_int64] + [_i32] * 4 + [_vp])
+        _bwd = _fn("mc_conv_gn_bwd", [_vp] * 16 + [ctypes.c_int64] + [_i32] * 5 + [_vp])
         _bwd_ws = _fn("mc_conv_gn_bwd_workspace", [_i32] * 4)
         _bwd_ws.restype = ctypes.c_int64
     n, p, cin = x.shape
     dev = x.device
+    dt, et = _dt(x), x.dtype
     assert out is not None or rmask is not None
     for t in (dout, out, y):
-        assert t is None or (t.shape == (n, p, COUT) and t.dtype == torch.bfloat16 and t.is_contiguous())
+        assert t is None or (t.shape == (n, p, COUT) and t.dtype == et and t.is_contiguous())
     if rmask is not None:
         assert rmask.shape == (n, p, COUT // 8) and rmask.dtype == torch.uint8 and rmask.is_contiguous()
-    assert x.dtype == torch.bfloat16 and x.is_contiguous() and p == H * W
+    assert x.is_contiguous() and p == H * W
     assert stats.shape == (n, NGROUPS, 2) and stats.dtype == torch.float32
     if wT is not None:
-        assert wT.shape == (9, cin, COUT) and wT.dtype == torch.bfloat16 and wT.is_contiguous()
+        assert wT.shape == (9, cin, COUT) and wT.dtype == et and wT.is_contiguous()
     if addend is not None:
-        assert addend.shape == (n, p, cin) and addend.dtype == torch.bfloat16 and addend.is_contiguous()
+        assert addend.shape == (n, p, cin) and addend.dtype == et and addend.is_contiguous()
     if dmask is not None:
         dmask = dmask.to(torch.float32).contiguous()
     g = gamma.detach().to(torch.float32).contiguous()
-    dy = torch.empty((n, p, COUT), dtype=torch.bfloat16, device=dev)
+    dy = torch.empty((n, p, COUT), dtype=et, device=dev)
     dz = torch.empty_like(dy) if want_dz else None
-    dx = torch.empty((n, p, cin), dtype=torch.bfloat16, device=dev) if wT is not None else None
+    dx = torch.empty((n, p, cin), dtype=et, device=dev) if wT is not None else None
     dw = torch.empty((9, COUT, cin), dtype=torch.float32, device=dev)
     dgn = torch.empty((3, COUT), dtype=torch.float32, device=dev)
     nws = int(_bwd_ws(n, H, W, cin))
@@ -138,7 +148,7 @@ def conv_gn_bwd(dout: torch.Tensor, out: Optional[torch.Tensor], y: torch.Tensor
     work = torch.empty(nws, dtype=torch.float32, device=dev)
     _check(_bwd(L.ptr(dout), L.ptr(out), L.ptr(rmask), L.ptr(y), L.ptr(stats), L.ptr(g), L.ptr(dmask), L.ptr(x), L.ptr(wT),
                 L.ptr(addend), L.ptr(dy), L.ptr(dz), L.ptr(dx), L.ptr(dw), L.ptr(dgn), L.ptr(work), nws,
-                n, H, W, cin, L.stream_ptr(dev)))
+                n, H, W, cin, dt, L.stream_ptr(dev)))
     return dx, dz, dw, dgn
 
 
@@ -151,16 +161,16 @@ def conv_gn_bwd(dout: torch.Tensor, out: Optional[torch.Tensor], y: torch.Tensor
 _wcache = WeakIdKeyDictionary()
 
 
-def _packed(w: torch.Tensor, kind: str, cin_pad: int = 0) -> torch.Tensor:
-    """bf16 re-layout of a conv weight, cached until the optimizer bumps its version."""
+def _packed(w: torch.Tensor, kind: str, dtype: torch.dtype, cin_pad: int = 0) -> torch.Tensor:
+    """16-bit re-layout of a conv weight, cached until the optimizer bumps its version."""
     ent = _wcache.get(w)
     if ent is None:
         ent = _wcache[w] = {}
-    hit = ent.get(kind)
+    hit = ent.get((kind, dtype))
     if hit is not None and hit[0] == w._version:
         return hit[1]
-    t = prep_weight(w.detach(), cin_pad) if kind == "f" else prep_weight_t(w.detach())
-    ent[kind] = (w._version, t)
+    t = prep_weight(w.detach(), cin_pad, dtype) if kind == "f" else prep_weight_t(w.detach(), dtype)
+    ent[(kind, dtype)] = (w._version, t)
     return t
 
 
@@ -178,7 +188,7 @@ def _trunk_forward(x0, layers, H, W, dmasks, save):
     acts, ys, sts, rms = [x0], [], [], []
     x, blk_in = x0, None
     for li, (conv, norm) in enumerate(layers):
-        wt = _packed(conv.weight, "f", x.shape[-1])
+        wt = _packed(conv.weight, "f", x.dtype, x.shape[-1])
         res = dm = None
         if li % 2 == 1:  # first half of a block: Dropout2d after the ReLU
             blk_in = x
@@ -212,7 +222,7 @@ class _TrunkFn(torch.autograd.Function):
         acts, ys, sts, rms = ctx.saved
         layers, H, W, dmasks = ctx.layers, ctx.H, ctx.W, ctx.dmasks
         grads = {}
-        d = dout.to(torch.bfloat16).contiguous()
+        d = dout.to(acts[0].dtype).contiguous()
         nl = len(layers)
         skip = None  # dz of a block's second half: the block input's skip gradient
         for li in range(nl - 1, -1, -1):
@@ -223,7 +233,7 @@ class _TrunkFn(torch.autograd.Function):
             dm = dmasks[(li - 1) // 2] if (dmasks is not None and li % 2 == 1) else None
             addend = skip if li % 2 == 1 else None
             dx, dz, dw, dgn = conv_gn_bwd(d, None, ys[li], sts[li], norm.weight, x, H, W,
-                                          wT=_packed(conv.weight, "t") if want_dx else None, dmask=dm,
+                                          wT=_packed(conv.weight, "t", x.dtype) if want_dx else None, dmask=dm,
                                           addend=addend, want_dz=(li % 2 == 0 and li > 0), rmask=rms[li])
             skip = dz
             grads[id(conv.weight)] = dw_to_conv(dw, cin_real)
@@ -244,12 +254,13 @@ def trunk_params(layers) -> list:
     return [p for conv, norm in layers for p in (conv.weight, conv.bias, norm.weight, norm.bias)]
 
 
-def fused_features(model, obs: torch.Tensor) -> torch.Tensor:
-    """Trunk features of CNNResidualPolicy as NHWC bf16 [N, H*W, 96] via the fused kernels.
-    Dropout2d masks are drawn here (torch RNG) when the model is in training mode."""
+def fused_features(model, obs: torch.Tensor, dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
+    """Trunk features of CNNResidualPolicy as NHWC ``dtype`` [N, H*W, 96] via the fused kernels
+    (``dtype``: the autocast type, bf16 or fp16). Dropout2d masks are drawn here (torch RNG)
+    when the model is in training mode."""
     n, c, H, W = obs.shape
     layers = trunk_layers(model)
-    x0 = obs_to_nhwc(obs, 16)
+    x0 = obs_to_nhwc(obs, 16, dtype)
     nblk = len(model.residual_stack)
     p = model.residual_stack[0].dropout.p if isinstance(model.residual_stack[0].dropout, torch.nn.Dropout2d) else 0.0
     dmasks = None
@@ -271,44 +282,46 @@ _hf = _hb = _hbws = None
 _hcache: dict = {}
 
 
-def _head_pack(pol, mine):
-    """bf16 [192|96, 96] W1 (policy rows first), its policy transpose, f32 b1 / w2 / b2."""
+def _head_pack(pol, mine, dtype: torch.dtype):
+    """``dtype`` [192|96, 96] W1 (policy rows first), its policy transpose, f32 b1 / w2 / b2."""
     heads = [pol] + ([mine] if mine is not None else [])
     params = tuple(t for h in heads for m in (h[0], h[2]) for t in (m.weight, m.bias))
     vers = tuple(t._version for t in params)
     # the entry holds the parameters themselves and compares by identity: ids of freed
     # parameters can be reused by a new model at the same versions
-    hit = _hcache.get(len(heads))
+    key = (len(heads), dtype)
+    hit = _hcache.get(key)
     if hit is not None and hit[1] == vers and all(a is b for a, b in zip(hit[0], params)):
         return hit[2]
-    w1 = torch.cat([h[0].weight.detach().reshape(COUT, COUT) for h in heads]).to(torch.bfloat16).contiguous()
-    w1pT = pol[0].weight.detach().reshape(COUT, COUT).t().to(torch.bfloat16).contiguous()
+    w1 = torch.cat([h[0].weight.detach().reshape(COUT, COUT) for h in heads]).to(dtype).contiguous()
+    w1pT = pol[0].weight.detach().reshape(COUT, COUT).t().to(dtype).contiguous()
     b1 = torch.cat([h[0].bias.detach() for h in heads]).float().contiguous()
     w2 = torch.cat([h[2].weight.detach().reshape(COUT) for h in heads]).float().contiguous()
     b2 = torch.cat([h[2].bias.detach().reshape(1) for h in heads]).float().contiguous()
     packed = (w1, w1pT, b1, w2, b2)
-    _hcache[len(heads)] = (params, vers, packed)
+    _hcache[key] = (params, vers, packed)
     return packed
 
 
 def _heads_bind():
     global _hf, _hb, _hbws
     if _hf is None:
-        _hf = _fn("mc_heads_fwd", [_vp] * 7 + [ctypes.c_int64, _vp])
-        _hb = _fn("mc_heads_bwd", [_vp] * 8 + [_i32] + [_vp] * 5 + [ctypes.c_int64, ctypes.c_int64, _vp])
+        _hf = _fn("mc_heads_fwd", [_vp] * 7 + [ctypes.c_int64, _i32, _vp])
+        _hb = _fn("mc_heads_bwd", [_vp] * 8 + [_i32] + [_vp] * 5 + [ctypes.c_int64, ctypes.c_int64, _i32, _vp])
         _hbws = _fn("mc_heads_bwd_workspace", [ctypes.c_int64])
         _hbws.restype = ctypes.c_int64
 
 
 def heads_forward(f: torch.Tensor, pol, mine=None):
-    """f bf16 [N, P, 96] -> policy logits f32 [N, P] (and mine logits f32 [N, P] when ``mine``)."""
+    """f bf16 | fp16 [N, P, 96] -> policy logits f32 [N, P] (and mine logits f32 [N, P] when ``mine``)."""
     _heads_bind()
     n, p, c = f.shape
-    assert c == COUT and f.dtype == torch.bfloat16 and f.is_contiguous()
-    w1, _, b1, w2, b2 = _head_pack(pol, mine)
+    dt = _dt(f)
+    assert c == COUT and f.is_contiguous()
+    w1, _, b1, w2, b2 = _head_pack(pol, mine, f.dtype)
     lp = torch.empty((n, p), dtype=torch.float32, device=f.device)
     lm = torch.empty_like(lp) if mine is not None else None
-    _check(_hf(L.ptr(f), L.ptr(w1), L.ptr(b1), L.ptr(w2), L.ptr(b2), L.ptr(lp), L.ptr(lm), n * p,
+    _check(_hf(L.ptr(f), L.ptr(w1), L.ptr(b1), L.ptr(w2), L.ptr(b2), L.ptr(lp), L.ptr(lm), n * p, dt,
                L.stream_ptr(f.device)))
     return lp, lm
 
@@ -333,7 +346,7 @@ class _HeadsFn(torch.autograd.Function):
         n, p, _ = f.shape
         M = n * p
         # the kernel always runs both heads' math; without a mine head its rows get dl = 0
-        w1, w1pT, b1, w2, _ = _head_pack(pol, mine if mine is not None else pol)
+        w1, w1pT, b1, w2, _ = _head_pack(pol, mine if mine is not None else pol, f.dtype)
         dev = f.device
         dlp = dlp.float().contiguous() if dlp is not None else torch.zeros(n, p, device=dev)
         dlm = dlm.float().contiguous() if (dlm is not None and mine is not None) else None
@@ -345,7 +358,7 @@ class _HeadsFn(torch.autograd.Function):
         nws = int(_hbws(M))
         work = torch.empty(nws, device=dev)
         _check(_hb(L.ptr(f), L.ptr(dlp), L.ptr(dlm), L.ptr(w1), L.ptr(w1pT), L.ptr(b1), L.ptr(w2), L.ptr(gadd), p,
-                   L.ptr(df), L.ptr(dw1), L.ptr(db1), L.ptr(dw2), L.ptr(work), nws, M, L.stream_ptr(dev)))
+                   L.ptr(df), L.ptr(dw1), L.ptr(db1), L.ptr(dw2), L.ptr(work), nws, M, _dt(f), L.stream_ptr(dev)))
         grads = [df, None, None]
         for h, i, dl in [(pol, 0, dlp)] + ([(mine, 1, dlm)] if mine is not None else []):
             sl = slice(i * COUT, (i + 1) * COUT)

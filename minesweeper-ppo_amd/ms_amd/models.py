@@ -95,7 +95,7 @@ class CNNResidualPolicy(nn.Module):
         )
         self.mine_head = _pointwise_head(C)
 
-        # fused MFMA trunk (csrc/mscnn*.hip) on HIP devices under bf16 autocast;
+        # fused MFMA trunk (csrc/mscnn*.hip) on HIP devices under bf16 or fp16 autocast;
         # MS_AMD_FUSED=0 forces the PyTorch op chain (A/B measurements)
         self.fused = os.environ.get("MS_AMD_FUSED", "1") != "0"
 
@@ -106,7 +106,7 @@ class CNNResidualPolicy(nn.Module):
         conv0 = self.stem[0]
         return (self.fused and x.is_cuda and conv0.out_channels == 96 and conv0.in_channels <= 16
                 and x.shape[2] * x.shape[3] <= 512 and torch.is_autocast_enabled("cuda")
-                and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+                and torch.get_autocast_dtype("cuda") in (torch.bfloat16, torch.float16))
 
     def features(self, x: torch.Tensor) -> torch.Tensor:
         return self.residual_stack(self.stem(x))
@@ -141,7 +141,8 @@ class CNNResidualPolicy(nn.Module):
     def forward(self, x: torch.Tensor, return_mine: bool = False):
         if self.use_fused(x):
             from .fused import fused_features
-            return self._heads_fused(fused_features(self, x), x.shape[2], x.shape[3], return_mine)
+            f = fused_features(self, x, torch.get_autocast_dtype("cuda"))
+            return self._heads_fused(f, x.shape[2], x.shape[3], return_mine)
         f = self.features(x)
         n = f.shape[0]
         # [N,1,H,W] -> [N,H*W], index r*W + c (cnn_residual.py:89)

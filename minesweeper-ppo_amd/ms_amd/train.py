@@ -301,7 +301,7 @@ def main(argv=None) -> None:
     ap.add_argument("--quick_eval_pairs", type=int, default=2)
     ap.add_argument("--quick_eval_interval", type=int, default=10)
     ap.add_argument("--eval_pairs", type=int, default=1)
-    ap.add_argument("--eval_amp", choices=["fp32", "bf16"], default="fp32",
+    ap.add_argument("--eval_amp", choices=["fp32", "bf16", "fp16"], default="fp32",
                     help="evaluation precision (the reference evaluates in fp32)")
     ap.add_argument("--skip_final_eval", action="store_true")
     ap.add_argument("--grad_checkpoint", action="store_true")
@@ -322,7 +322,7 @@ def main(argv=None) -> None:
     tr = Trainer(cfg, env_d, model_d, extras, seed=args.seed, model_name=args.model, info=info, amp=args.amp,
                  device=device)
     env_cfg = tr.vec.cfg
-    eval_amp = torch.bfloat16 if args.eval_amp == "bf16" else None
+    eval_amp = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(args.eval_amp)
     if args.init_ckpt:
         tr.load_init(args.init_ckpt)
     if info.is_main:

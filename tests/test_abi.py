@@ -54,9 +54,18 @@ def test_cnn_entry_points_validate_arguments():
     assert lib.mc_conv_gn_bwd_workspace(0, 16, 16, 96) == -1
     assert lib.mc_conv_gn_bwd_workspace(4, 16, 16, 32) == -1  # cin 16 or 96 only
     vp = ctypes.c_void_p
-    lib.mc_conv_gn_fwd.argtypes = [vp] * 11 + [ctypes.c_int32] * 4 + [ctypes.c_float, vp]
-    assert lib.mc_conv_gn_fwd(*([None] * 11), 4, 16, 16, 96, 1e-5, None) == 1
+    i32 = ctypes.c_int32
+    lib.mc_conv_gn_fwd.argtypes = [vp] * 11 + [i32] * 4 + [ctypes.c_float, i32, vp]
+    assert lib.mc_conv_gn_fwd(*([None] * 11), 4, 16, 16, 96, 1e-5, 0, None) == 1
     assert b"bad argument" in lib.mc_last_error()
+    # an unknown element type (include/mscnn.h: MC_DTYPE_BF16 0, MC_DTYPE_F16 1) is refused
+    # before anything touches the device (the pointers are never dereferenced)
+    fake = [vp(4096)] * 5 + [None, None, vp(4096), None, None, None]
+    assert lib.mc_conv_gn_fwd(*fake, 4, 16, 16, 96, 1e-5, 2, None) == 1
+    assert b"dtype 2" in lib.mc_last_error()
+    lib.mc_heads_fwd.argtypes = [vp] * 7 + [ctypes.c_int64, i32, vp]
+    assert lib.mc_heads_fwd(*([vp(4096)] * 6), None, 256, 7, None) == 1
+    assert b"dtype 7" in lib.mc_last_error()
 
 
 def test_single_hip_runtime_mapped():

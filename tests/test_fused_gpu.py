@@ -1,6 +1,8 @@
 """Fused conv3x3 + GroupNorm + residual + ReLU + dropout MFMA kernel vs a
-PyTorch fp32 reference of the same op on the same bf16-rounded inputs.
-Tolerance: |d| <= 2e-2 + 2e-2*|ref| (bf16 output rounding is 2^-8 relative)."""
+PyTorch fp32 reference of the same op on the same 16-bit-rounded inputs, for both
+element types (bf16, and fp16 = the reference's autocast type).
+Tolerance: |d| <= 2e-2 + 2e-2*|ref| (bf16 output rounding is 2^-8 relative; fp16's
+2^-11 passes the same bounds)."""
 from __future__ import annotations
 
 import pytest
@@ -10,10 +12,13 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 
+DT = [torch.bfloat16, torch.float16]
+
+
 def _ref(x, w, b, g, be, H, W, res=None, dmask=None):
     n, p, cin = x.shape
     xin = x.float().view(n, H, W, cin).permute(0, 3, 1, 2)
-    wf = w.to(torch.bfloat16).float()
+    wf = w.to(x.dtype).float()
     y = F.conv2d(xin, wf[:, :cin] if wf.shape[1] >= cin else wf, b, padding=1)
     z = F.group_norm(y, 6, g, be, eps=1e-5)
     if res is not None:
@@ -31,20 +36,22 @@ def _ref(x, w, b, g, be, H, W, res=None, dmask=None):
 @pytest.mark.parametrize("H,W,cin,n", [(16, 16, 96, 300), (16, 16, 16, 37), (9, 9, 96, 70), (30, 16, 96, 20),
                                        (16, 30, 96, 9), (5, 7, 16, 3)])
 @pytest.mark.parametrize("with_res", [False, True])
-def test_conv_gn_fwd_matches_torch(gpu, H, W, cin, n, with_res):
+@pytest.mark.parametrize("dt", DT)
+def test_conv_gn_fwd_matches_torch(gpu, H, W, cin, n, with_res, dt):
     """The fused forward (conv + bias + GroupNorm + affine [+ residual] + ReLU [+ dropout
     scale]) and its ReLU bitmask vs a torch fp32 reference of the same op."""
     from ms_amd.fused import conv_gn_fwd, prep_weight
     torch.manual_seed(0)
     P = H * W
-    x = (torch.randn(n, P, cin, device=gpu) * (0.5 if cin == 96 else 1.0)).to(torch.bfloat16)
+    x = (torch.randn(n, P, cin, device=gpu) * (0.5 if cin == 96 else 1.0)).to(dt)
     if cin == 16:
         x[:, :, 10:] = 0  # stem: 10 obs planes zero-padded to 16
     w = torch.randn(96, cin, 3, 3, device=gpu) * (1.0 / (3 * cin ** 0.5))
     b, g, be = torch.randn(96, device=gpu) * 0.1, 1 + 0.1 * torch.randn(96, device=gpu), 0.1 * torch.randn(96, device=gpu)
-    res = torch.randn(n, P, 96, device=gpu).to(torch.bfloat16) if with_res else None
+    res = torch.randn(n, P, 96, device=gpu).to(dt) if with_res else None
     dmask = ((torch.rand(n, 96, device=gpu) > 0.05).float() / 0.95) if not with_res else None
-    out, y, st, rm = conv_gn_fwd(x, prep_weight(w, cin), b, g, be, H, W, res=res, dmask=dmask, want_mask=True)
+    out, y, st, rm = conv_gn_fwd(x, prep_weight(w, cin, dt), b, g, be, H, W, res=res, dmask=dmask, want_mask=True)
+    assert out.dtype == dt and y.dtype == dt
     ro, ry, rst = _ref(x, w, b, g, be, H, W, res, dmask)
     torch.testing.assert_close(y.float(), ry, atol=2e-2, rtol=2e-2)
     torch.testing.assert_close(st, rst, atol=1e-3, rtol=1e-3)
@@ -68,7 +75,8 @@ def _gn(y, g, b):
 @pytest.mark.parametrize("H,W,cin,n", [(16, 16, 96, 300), (16, 16, 16, 37), (9, 9, 96, 70), (30, 16, 96, 20),
                                        (5, 7, 16, 3), (8, 8, 96, 5), (16, 16, 96, 600)])
 @pytest.mark.parametrize("with_res", [False, True])
-def test_conv_gn_bwd_matches_torch(gpu, H, W, cin, n, with_res):
+@pytest.mark.parametrize("dt", DT)
+def test_conv_gn_bwd_matches_torch(gpu, H, W, cin, n, with_res, dt):
     """Fused backward (GroupNorm backward + dgrad + wgrad) vs torch fp32 autograd.
 
     Tight check: the reference starts from the SAVED bf16 conv output y (what the
@@ -79,22 +87,23 @@ def test_conv_gn_bwd_matches_torch(gpu, H, W, cin, n, with_res):
     from ms_amd.fused import conv_gn_bwd, conv_gn_fwd, dw_to_conv, prep_weight, prep_weight_t
     torch.manual_seed(1)
     P = H * W
-    x = (torch.randn(n, P, cin, device=gpu) * (0.5 if cin == 96 else 1.0)).to(torch.bfloat16)
+    x = (torch.randn(n, P, cin, device=gpu) * (0.5 if cin == 96 else 1.0)).to(dt)
     if cin == 16:
         x[:, :, 10:] = 0
-    w = (torch.randn(96, cin, 3, 3, device=gpu) * (1.0 / (3 * cin ** 0.5))).to(torch.bfloat16).float()
+    w = (torch.randn(96, cin, 3, 3, device=gpu) * (1.0 / (3 * cin ** 0.5))).to(dt).float()
     b, g, be = torch.randn(96, device=gpu) * 0.1, 1 + 0.1 * torch.randn(96, device=gpu), 0.1 * torch.randn(96, device=gpu)
-    res = torch.randn(n, P, 96, device=gpu).to(torch.bfloat16) if with_res else None
+    res = torch.randn(n, P, 96, device=gpu).to(dt) if with_res else None
     dmask = ((torch.rand(n, 96, device=gpu) > 0.1).float() / 0.9) if not with_res else None
-    out, y, st = conv_gn_fwd(x, prep_weight(w, cin), b, g, be, H, W, res=res, dmask=dmask)
-    dout = torch.randn(n, P, 96, device=gpu).to(torch.bfloat16)
+    out, y, st = conv_gn_fwd(x, prep_weight(w, cin, dt), b, g, be, H, W, res=res, dmask=dmask)
+    dout = torch.randn(n, P, 96, device=gpu).to(dt)
     want_dx = cin == 96
-    add = torch.randn(n, P, cin, device=gpu).to(torch.bfloat16) if (with_res and want_dx) else None
-    dx, dz, dw, dgn = conv_gn_bwd(dout, out, y, st, g, x, H, W, wT=prep_weight_t(w) if want_dx else None,
+    add = torch.randn(n, P, cin, device=gpu).to(dt) if (with_res and want_dx) else None
+    dx, dz, dw, dgn = conv_gn_bwd(dout, out, y, st, g, x, H, W, wT=prep_weight_t(w, dt) if want_dx else None,
                                   dmask=dmask, addend=add, want_dz=with_res)
+    assert dx is None or dx.dtype == dt
     # the bitmask path (what the trunk uses) gives bit-identical gradients
-    rm = conv_gn_fwd(x, prep_weight(w, cin), b, g, be, H, W, res=res, dmask=dmask, want_mask=True)[3]
-    got = conv_gn_bwd(dout, None, y, st, g, x, H, W, wT=prep_weight_t(w) if want_dx else None,
+    rm = conv_gn_fwd(x, prep_weight(w, cin, dt), b, g, be, H, W, res=res, dmask=dmask, want_mask=True)[3]
+    got = conv_gn_bwd(dout, None, y, st, g, x, H, W, wT=prep_weight_t(w, dt) if want_dx else None,
                       dmask=dmask, addend=add, want_dz=with_res, rmask=rm)
     for a_, b_ in zip((dx, dz, dw, dgn), got):
         assert (a_ is None and b_ is None) or torch.equal(a_, b_)
@@ -143,7 +152,8 @@ def test_conv_gn_bwd_matches_torch(gpu, H, W, cin, n, with_res):
 
 @pytest.mark.parametrize("n,P", [(300, 256), (7, 81), (3, 30)])
 @pytest.mark.parametrize("with_mine", [True, False])
-def test_heads_match_torch(gpu, n, P, with_mine):
+@pytest.mark.parametrize("dt", DT)
+def test_heads_match_torch(gpu, n, P, with_mine, dt):
     """Policy + mine heads (csrc/msheads.hip) and the pooled features vs a torch fp32
     reference on the same bf16 features; gradients of f (policy path + pool only: the
     mine head reads f.detach()) and of every head parameter. Relative L2 <= 1e-2."""
@@ -152,7 +162,7 @@ def test_heads_match_torch(gpu, n, P, with_mine):
     mk = lambda: torch.nn.Sequential(torch.nn.Conv2d(96, 96, 1), torch.nn.ReLU(),  # noqa: E731
                                      torch.nn.Conv2d(96, 1, 1)).to(gpu)
     pol, mine = mk(), mk()
-    f = (torch.randn(n, P, 96, device=gpu) * 0.7).to(torch.bfloat16).requires_grad_(True)
+    f = (torch.randn(n, P, 96, device=gpu) * 0.7).to(dt).requires_grad_(True)
     wl, wp, wm = torch.randn(n, P, device=gpu), torch.randn(n, 96, device=gpu), torch.randn(n, P, device=gpu)
     lp, pooled, lm = heads_apply(f, pol, mine if with_mine else None)
     loss = (lp * wl).sum() + (pooled * wp).sum() + ((lm * wm).sum() if with_mine else 0)
@@ -162,8 +172,8 @@ def test_heads_match_torch(gpu, n, P, with_mine):
     for mod in (pol, mine):
         mod.zero_grad(set_to_none=True)
     fr = f.detach().float().requires_grad_(True)
-    # the kernel's W1 is bf16 (as under the reference's autocast): round it the same way
-    bfw = lambda w: w + (w.detach().to(torch.bfloat16).float() - w.detach())  # noqa: E731  (grad flows to w)
+    # the kernel's W1 is 16-bit (as under the reference's autocast): round it the same way
+    bfw = lambda w: w + (w.detach().to(dt).float() - w.detach())  # noqa: E731  (grad flows to w)
     lin = lambda h, t: torch.nn.functional.linear(  # noqa: E731
         torch.relu(torch.nn.functional.linear(t, bfw(h[0].weight.flatten(1)), h[0].bias)), h[2].weight.flatten(1),
         h[2].bias).squeeze(-1)

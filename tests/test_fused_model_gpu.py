@@ -1,7 +1,7 @@
-"""CNNResidualPolicy through the fused MFMA trunk (bf16 autocast) vs the same
+"""CNNResidualPolicy through the fused MFMA trunk (bf16 or fp16 autocast) vs the same
 model through PyTorch fp32 ops: outputs and every parameter gradient.
-Tolerance: relative L2 error <= max(4e-2, 2 x the error of PyTorch's own bf16
-autocast path, which is what the reference trains with)."""
+Tolerance: relative L2 error <= max(4e-2, 2 x the error of PyTorch's own autocast
+path of the same type; fp16 is what the reference trains with)."""
 from __future__ import annotations
 
 import pytest
@@ -21,7 +21,8 @@ def _obs(n, H, W, dev):
 
 
 @pytest.mark.parametrize("H,W,n,blocks", [(16, 16, 300, 2), (9, 9, 64, 1), (30, 16, 40, 2)])
-def test_fused_model_matches_fp32(gpu, H, W, n, blocks):
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_fused_model_matches_fp32(gpu, H, W, n, blocks, dt):
     from ms_amd.models import CNNResidualPolicy
     torch.manual_seed(0)
     m = CNNResidualPolicy(10, stem_channels=96, blocks=blocks, dropout=0.05, value_hidden=64).to(gpu).eval()
@@ -32,7 +33,7 @@ def test_fused_model_matches_fp32(gpu, H, W, n, blocks):
         amp = fused if amp is None else amp
         m.fused = fused
         m.zero_grad(set_to_none=True)
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+        with torch.autocast("cuda", dtype=dt, enabled=amp):
             assert m.use_fused(obs) == fused
             lo, v, mi = m(obs, return_mine=True)
             loss = (lo.float() * wl).sum() + (v.float() * wv).sum() + (mi.float() * wm).sum()
@@ -40,7 +41,7 @@ def test_fused_model_matches_fp32(gpu, H, W, n, blocks):
         return lo.float(), v.float(), mi.float(), {k: p.grad.clone() for k, p in m.named_parameters()}
 
     lr, vr, mr, gr = run(False)
-    lb, vb, mb, gb = run(False, amp=True)  # PyTorch bf16 autocast
+    lb, vb, mb, gb = run(False, amp=True)  # PyTorch autocast of the same type
     lf, vf, mf, gf = run(True)
     tol = lambda ref_err: max(4e-2, 2.0 * ref_err)  # noqa: E731
     for a, b, r in ((lf, lb, lr), (vf, vb, vr), (mf, mb, mr)):

@@ -48,7 +48,7 @@ def _full(H, W, dev, dropout=0.05):
 
 
 def _fwd(m, obs, amp=None):
-    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp is not None):
+    with torch.no_grad(), torch.autocast("cuda", dtype=amp or torch.bfloat16, enabled=amp is not None):
         lg, v, mi = m(obs, return_mine=True)
     return lg.float().cpu().numpy(), v.float().cpu().numpy(), mi.float().cpu().numpy()
 
@@ -83,23 +83,26 @@ def test_small_and_cnn_models_fp32_on_device(gpu):
         np.testing.assert_allclose(a, z[k], rtol=0, atol=1e-5, err_msg=k)
 
 
-# bf16 bound for whole-model outputs (fused path and PyTorch bf16 autocast vs fp32 reference)
+# 16-bit bound for whole-model outputs (fused path and PyTorch autocast vs fp32 reference)
 BF16_OUT_FLOOR = 2e-2
 
 
 @pytest.mark.parametrize("H,W", [(16, 16), (9, 9), (30, 16)])
-def test_full_model_fused_bf16_matches_reference(gpu, H, W):
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16], ids=["bf16", "fp16"])
+def test_full_model_fused_bf16_matches_reference(gpu, H, W, dt):
+    """Fused trunk + heads under bf16 and under fp16 (the reference's autocast type) vs the
+    reference's fp32 outputs: within max(2e-2, 2 x PyTorch's own autocast error)."""
     z = golden(f"model_full_{H}x{W}.npz")
     m = _full(H, W, gpu).eval()
     obs = torch.from_numpy(z["obs"]).to(gpu)
-    with torch.autocast("cuda", dtype=torch.bfloat16):
+    with torch.autocast("cuda", dtype=dt):
         assert m.use_fused(obs)
-    fused = _fwd(m, obs, amp=True)
+    fused = _fwd(m, obs, amp=dt)
     m.fused = False
-    torch_bf16 = _fwd(m, obs, amp=True)
+    torch_amp = _fwd(m, obs, amp=dt)
     for i, k in enumerate(("logits", "value", "mine")):
-        e_f, e_t = _rel(fused[i], z[k]), _rel(torch_bf16[i], z[k])
-        print(f"{H}x{W} {k}: fused {e_f:.3e} torch-bf16 {e_t:.3e}")
+        e_f, e_t = _rel(fused[i], z[k]), _rel(torch_amp[i], z[k])
+        print(f"{H}x{W} {dt} {k}: fused {e_f:.3e} torch-autocast {e_t:.3e}")
         assert e_f <= max(BF16_OUT_FLOOR, 2 * e_t), (k, e_f, e_t)
 
 
@@ -210,9 +213,12 @@ def test_ppo_update_full_fp32_on_device(gpu, flat):
     _check_adamw_step({k: v.detach().cpu() for k, v in m.state_dict().items()}, z, g_ref, grads)
 
 
-def test_ppo_update_full_fused_bf16_trainer_path(gpu):
-    """The Trainer's path: bf16 autocast, fused MFMA trunk + heads, FlatGrads, no scaler.
-    Gradients within max(5e-2, 2 x PyTorch-bf16-autocast error) per tensor of the reference's
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16], ids=["bf16", "fp16"])
+def test_ppo_update_full_fused_bf16_trainer_path(gpu, dt):
+    """The Trainer's path: bf16 autocast without a scaler, or fp16 autocast with a GradScaler
+    (the reference's ppo.py:25 / train_rl.py:415-420 path; init_scale 2^10 so that the
+    first step is not skipped for overflow), fused MFMA trunk + heads, FlatGrads.
+    Gradients within max(5e-2, 2 x PyTorch-autocast error) per tensor of the reference's
     fp32 gradients; loss terms within 2e-2 relative."""
     from ms_amd.ppo import FlatGrads, PPOConfig, ppo_update
     cfg = PPOConfig(ent_coef=0.003, aux_mine_weight=0.05, aux_mine_calib_weight=0.01)
@@ -224,16 +230,18 @@ def test_ppo_update_full_fused_bf16_trainer_path(gpu):
         grads = _record_grads(m, opt)
         b = _batch(z, gpu)
         if fused:
-            with torch.autocast("cuda", dtype=torch.bfloat16):
+            with torch.autocast("cuda", dtype=dt):
                 assert m.use_fused(b.obs)
-        stats = ppo_update(m, opt, b, cfg, scaler=None, amp_dtype=torch.bfloat16,
+        scaler = torch.amp.GradScaler("cuda", init_scale=2.0 ** 10) if dt == torch.float16 else None
+        stats = ppo_update(m, opt, b, cfg, scaler=scaler, amp_dtype=dt,
                            flat_grads=FlatGrads(m.parameters()))
+        assert len(grads) > 0  # the optimizer stepped (no overflow skip)
         res[fused] = (stats, grads, {k: v.detach().cpu() for k, v in m.state_dict().items()})
     ref = dict(zip(z["stat_names"].tolist(), z["stat_values"].tolist()))
     stats, grads, post = res[True]
     for k in ("loss", "policy_loss", "value_loss", "entropy", "aux_bce", "aux_calib"):
         e = abs(stats[k] - ref[k]) / max(abs(ref[k]), 1e-3)
-        print(f"stat {k}: fused {stats[k]:.6f} ref {ref[k]:.6f} rel {e:.2e} torch-bf16 {res[False][0][k]:.6f}")
+        print(f"stat {k}: fused {stats[k]:.6f} ref {ref[k]:.6f} rel {e:.2e} torch-autocast {res[False][0][k]:.6f}")
         assert e < 2e-2, k
     worst = 0.0
     for k in grads:

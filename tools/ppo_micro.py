@@ -56,6 +56,7 @@ amp = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": None}[args.amp]
 if args.pure_bf16:
     amp = None
     b.mine_labels = b.mine_labels.bfloat16()
+scaler = torch.amp.GradScaler("cuda") if amp == torch.float16 else None  # the reference's fp16 path
 
 
 def step():
@@ -63,7 +64,7 @@ def step():
         with torch.no_grad(), torch.autocast("cuda", dtype=amp, enabled=amp is not None):
             m(obs)
     else:
-        ppo_update(m, opt, b, cfg, amp_dtype=amp, sync_stats=False)
+        ppo_update(m, opt, b, cfg, scaler, amp_dtype=amp, sync_stats=False)
 
 
 for _ in range(2):

@@ -70,7 +70,8 @@ def parse():
     ap.add_argument("--ppo-updates", type=int, default=2,
                     help="timed combined rollout+GAE+PPO updates (0 disables; +1 untimed warm-up)")
     ap.add_argument("--ppo-steps-per-env", type=int, default=64)
-    ap.add_argument("--amp", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--amp", default="fp16", choices=["bf16", "fp16", "fp32"],
+                    help="PPO autocast type (fp16 + GradScaler = the reference's training precision)")
     return ap.parse_args()
 
 
@@ -209,7 +210,7 @@ def multistep_bench(args, world, lib, h, L, n_local, n_total, H, W, bpe, dev):
 
 # fwd / fwd+bwd GFLOP per 16x16 sample of the shipped model (torch flop counter)
 GFLOP_FWD_16, GFLOP_FWDBWD_16 = 0.4388, 1.3073
-BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16
+BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 / fp16
 
 
 def ppo_kernel_profile():

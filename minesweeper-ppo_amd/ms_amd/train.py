@@ -141,7 +141,7 @@ class Trainer:
     update. Used by main() and by bench.py's combined-loop measurement."""
 
     def __init__(self, cfg: PPOTrainConfig, env_d: Dict, model_d: Dict, extras: Dict, *, seed: int = 0,
-                 model_name: str | None = None, info: DistInfo | None = None, amp: str = "bf16",
+                 model_name: str | None = None, info: DistInfo | None = None, amp: str = "fp16",
                  device: torch.device | None = None):
         self.cfg = cfg
         self.info = info or DistInfo()
@@ -293,7 +293,8 @@ def main(argv=None) -> None:
     ap.add_argument("--updates", type=int, default=None)
     ap.add_argument("--init_ckpt", type=str, default=None)
     ap.add_argument("--save_every", type=int, default=50)
-    ap.add_argument("--amp", choices=["bf16", "fp16", "fp32"], default="bf16")
+    ap.add_argument("--amp", choices=["bf16", "fp16", "fp32"], default="fp16",
+                    help="autocast type: fp16 + GradScaler as the reference (train_rl.py:415-420), bf16 (no scaler) or fp32")
     # evaluation flags of train_rl.py:297-305 (on-device greedy eval, ms_amd/eval.py)
     ap.add_argument("--eval_episodes", type=int, default=2048)
     ap.add_argument("--eval_num_envs", type=int, default=64)

@@ -107,15 +107,20 @@ def test_collect_rollout_replays_through_oracle(gpu):
     assert bool(buf.action_mask.gather(1, buf.actions[:, None]).all())
 
 
-def test_trainer_update_runs(gpu):
+@pytest.mark.parametrize("amp", ["fp16", "bf16"])
+def test_trainer_update_runs(gpu, amp):
+    """Trainer updates under the default fp16 autocast + GradScaler (the reference's) and
+    under bf16: finite stats, parameters move. A GradScaler step skipped for overflow (its
+    scale then halves) is the reference's behaviour too, so 4 updates leave room for it."""
     from ms_amd.train import Trainer, load_config
     import os
     cfg, env_d, model_d, extras = load_config(os.path.join(ROOT, "configs", "16x16x40_medium.yaml"))
     cfg.num_envs, cfg.steps_per_env, cfg.total_updates = 256, 8, 4
     model_d = dict(model_d, stem_channels=32, blocks=2, value_hidden=32)
-    tr = Trainer(cfg, env_d, model_d, extras, seed=0, device=gpu)
+    tr = Trainer(cfg, env_d, model_d, extras, seed=0, device=gpu, amp=amp)
+    assert (tr.scaler is not None) == (amp == "fp16")
     before = [p.detach().clone() for p in tr.model.parameters()]
-    for u in range(2):
+    for u in range(4):
         st = tr.update(u)
         assert all(np.isfinite(v) for v in st.values()), st
         assert {"loss", "policy_loss", "value_loss", "entropy", "aux_bce", "aux_calib"} <= set(st)

@@ -1,6 +1,6 @@
 """Micro-benchmark of one PPO minibatch update (fwd+bwd+AdamW) of the shipped
 model on synthetic 16x16 observations: where does the combined loop's time go?
-    python tools/ppo_micro.py --mb 32768 [--channels-last] [--benchmark] [--amp bf16]
+    python tools/ppo_micro.py --mb 32768 [--channels-last] [--benchmark] [--amp fp16|bf16|fp32]
 """
 import argparse
 import os
@@ -16,7 +16,7 @@ ap.add_argument("--mb", type=int, default=32768)
 ap.add_argument("--iters", type=int, default=6)
 ap.add_argument("--channels-last", action="store_true")
 ap.add_argument("--benchmark", action="store_true")
-ap.add_argument("--amp", default="bf16")
+ap.add_argument("--amp", default="fp16")
 ap.add_argument("--fwd-only", action="store_true")
 ap.add_argument("--pure-bf16", action="store_true", help="model + obs in bf16, no autocast (timing only)")
 args = ap.parse_args()

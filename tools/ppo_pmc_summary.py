@@ -8,7 +8,49 @@ import csv
 import glob
 import json
 import os
+import re
 from collections import defaultdict
+
+
+def label(name):
+    """'k_bwd_data<bf16, 2, true, 13, true>' from a rocprofv3 kernel name: demangled
+    ('(anonymous namespace)::k_bwd_data<2, true, ...>(...)') or, for the element-type
+    templates rocprofv3 leaves mangled, '_ZN12_GLOBAL__N_110k_bwd_dataIDF16b...'."""
+    if name.startswith("_ZN12_GLOBAL__N_1"):
+        rest = name[len("_ZN12_GLOBAL__N_1"):]
+        m = re.match(r"(\d+)", rest)
+        n = int(m.group(1))
+        base, rest = rest[len(m.group(1)):len(m.group(1)) + n], rest[len(m.group(1)) + n:]
+        args = []
+        if rest.startswith("I"):
+            i = 1
+            while i < len(rest) and rest[i] != "E":
+                if rest.startswith("DF16b", i):
+                    args.append("bf16"); i += 5
+                elif rest.startswith("DF16_", i):
+                    args.append("f16"); i += 5
+                elif rest.startswith("Lb", i):
+                    args.append("true" if rest[i + 2] == "1" else "false"); i += 4
+                elif rest.startswith("Li", i):
+                    j = rest.index("E", i)
+                    args.append(rest[i + 2:j]); i = j + 1
+                else:
+                    break
+        return f"{base}<{', '.join(args)}>" if args else base
+    short = name.split("(anonymous namespace)::", 1)[-1]
+    return re.match(r"\w+(<[^()]*>)?", short).group(0)
+
+
+def layer96(lab):
+    """the 96 -> 96 layers: forward / wgrad instantiated for 96 input channels, k_bwd_data's
+    data-gradient variant (template argument DGRAD = true; the stem's has no dgrad)"""
+    m = re.match(r"(\w+)<(.*)>$", lab)
+    if not m:
+        return False
+    args = [a.strip() for a in m.group(2).split(",") if a.strip() not in ("bf16", "f16")]
+    if m.group(1) in ("k_conv_gn_fwd", "k_wgrad"):
+        return args[0] == "96"
+    return m.group(1) == "k_bwd_data" and args[1] == "true"
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--fetch", required=True)
@@ -31,7 +73,7 @@ def counters(d, name):
                 continue
             key = r.get("Dispatch_Id", r.get("Correlation_Id"))
             acc[key] += float(r["Counter_Value"])
-            kern[key] = r["Kernel_Name"]
+            kern[key] = label(r["Kernel_Name"])
         for k, v in acc.items():
             per[kern[k]].append(v)
     return {k: sum(v) / len(v) for k, v in per.items()}
@@ -40,7 +82,7 @@ def counters(d, name):
 dur = defaultdict(list)
 for f in glob.glob(os.path.join(a.trace, "**", "*kernel_trace.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
-        dur[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        dur[label(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 fe, wr = counters(a.fetch, "FETCH_SIZE"), counters(a.write, "WRITE_SIZE")
 mb, gui = counters(a.mfma, "SQ_VALU_MFMA_BUSY_CYCLES"), counters(a.mfma, "GRBM_GUI_ACTIVE")
 flops96 = 2.0 * a.samples * a.pixels * 96 * 96 * 9
@@ -57,10 +99,7 @@ for k, ds in dur.items():
            "fetch_doubled": wide}
     if k in mb and gui.get(k):
         rec["mfma_busy_frac"] = mb[k] / (gui[k] / 8.0 * 1024.0)
-    # the 96 -> 96 layers: forward / wgrad instantiated for 96 input channels, k_bwd_data's
-    # data-gradient variant (template argument DGRAD = true; the stem's has no dgrad)
-    if ("k_conv_gn_fwd<96" in k or "k_wgrad<96" in k or "k_bwd_data<2, true" in k or "k_bwd_data<1, true" in k
-            or "k_bwd_data<3, true" in k or "k_bwd_data<4, true" in k):
+    if layer96(k):
         rec["algo_tflop"] = flops96 / 1e12
         rec["achieved_TFLOPs"] = flops96 / (us * 1e-6) / 1e12
         rec["mfma_frac_of_2500"] = rec["achieved_TFLOPs"] / 2500.0

@@ -982,32 +982,58 @@ __device__ __forceinline__ int select_bit64(uint64_t x, uint32_t k) {  // k-th s
   return pos;
 }
 
+// x mod c for c <= 65535 in 32-bit arithmetic (a 64-bit remainder is a long
+// software sequence on the GPU): x = hi * 2^32 + lo, 2^32 mod c = (2^32 - c) mod c
+__device__ __forceinline__ uint32_t mod64_small(uint64_t x, uint32_t c) {
+  const uint32_t hi = (uint32_t)(x >> 32), lo = (uint32_t)x;
+  const uint32_t r = ((hi % c) * ((0u - c) % c)) % c;  // < c^2 < 2^32
+  return (r + lo % c) % c;                              // < 2c
+}
+
+// The launch is one short dependency chain per lane (a load round trip, ~100 ALU
+// instructions), so its time is latency: one-wave workgroups spread the waves over
+// as many CUs as possible, the board words are loaded once (16-B loads) and kept in
+// registers, and the remainder is 32-bit.
 template <int H_, int W_>
-__global__ __launch_bounds__(256) void k_tape(const uint64_t* mw, const uint64_t* rw, int64_t n, int H_rt, int W_rt,
-                                              int64_t env_begin, uint64_t t, int mode, int64_t* actions) {
-  const int64_t env = (int64_t)blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(64) void k_tape(const uint64_t* mw, const uint64_t* rw, int64_t n, int H_rt, int W_rt,
+                                             int64_t env_begin, uint64_t t, int mode, int64_t* actions) {
+  const int64_t env = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (env >= n) return;
   const Geo<H_, W_> g(H_rt, W_rt);
   const int W = g.W, rpw = g.RPW(), NW = g.NW();
   constexpr int kNW = (H_ && W_) ? (H_ + (64 / W_) - 1) / (64 / W_) : 64;
+  constexpr bool kStatic = H_ && W_;
   const bool safe_mode = mode == MS_TAPE_SAFE_BIASED;
   const uint64_t* rp = rw + env * NW;
   const uint64_t* mp = mw + env * NW;
-  // word w of the valid (or safe) plane; loads are re-issued by the select pass
-  // (L1/L2 hits) rather than kept in an NW-long register array
-  auto plane = [&](int w, bool safe_plane) -> uint64_t {
+  auto valid_mask = [&](int w) -> uint64_t {
     const int rows = min(rpw, g.H - w * rpw);
     const int bits = rows * W;
-    const uint64_t wm = bits >= 64 ? ~0ull : ((1ull << bits) - 1ull);
-    const uint64_t v = ~rp[w] & wm;
-    return safe_plane ? (v & ~mp[w]) : v;
+    return bits >= 64 ? ~0ull : ((1ull << bits) - 1ull);
   };
+  uint64_t vw[kStatic ? kNW : 1], sw[kStatic ? kNW : 1];
   uint32_t n_valid = 0, n_safe = 0;
+  if constexpr (kStatic) {
+    // all loads first: the words of a board are contiguous (NW * 8 bytes)
+    uint64_t rr[kNW], mm[kNW];
 #pragma unroll
-  for (int w = 0; w < kNW; ++w) {
-    if (w < NW) {
-      n_valid += (uint32_t)__popcll(plane(w, false));
-      if (safe_mode) n_safe += (uint32_t)__popcll(plane(w, true));
+    for (int w = 0; w < kNW; ++w) rr[w] = rp[w];
+    if (safe_mode) {
+#pragma unroll
+      for (int w = 0; w < kNW; ++w) mm[w] = mp[w];
+    }
+#pragma unroll
+    for (int w = 0; w < kNW; ++w) {
+      vw[w] = ~rr[w] & valid_mask(w);
+      n_valid += (uint32_t)__popcll(vw[w]);
+      sw[w] = safe_mode ? (vw[w] & ~mm[w]) : 0ull;
+      n_safe += (uint32_t)__popcll(sw[w]);
+    }
+  } else {
+    for (int w = 0; w < NW; ++w) {
+      const uint64_t v = ~rp[w] & valid_mask(w);
+      n_valid += (uint32_t)__popcll(v);
+      if (safe_mode) n_safe += (uint32_t)__popcll(v & ~mp[w]);
     }
   }
   const uint64_t gidx = (uint64_t)(env_begin + env);
@@ -1017,17 +1043,33 @@ __global__ __launch_bounds__(256) void k_tape(const uint64_t* mw, const uint64_t
   const uint64_t sel = safe_mode ? (x >> 16) : x;
   int64_t act = 0;
   if (cnt > 0) {
-    uint32_t target = (uint32_t)(sel % (uint64_t)cnt);
+    uint32_t target = mod64_small(sel, cnt);
+    if constexpr (kStatic) {
 #pragma unroll
-    for (int w = 0; w < kNW; ++w) {
-      if (w < NW && target != 0xFFFFFFFFu) {
-        const uint64_t b = plane(w, want_safe);
+      for (int w = 0; w < kNW; ++w) {
+        if (target != 0xFFFFFFFFu) {
+          const uint64_t b = want_safe ? sw[w] : vw[w];
+          const uint32_t pc = (uint32_t)__popcll(b);
+          if (target < pc) {
+            const int pos = select_bit64(b, target);
+            const int r = w * rpw + pos / W;
+            act = (int64_t)r * W + (pos - (pos / W) * W);
+            target = 0xFFFFFFFFu;  // found
+          } else {
+            target -= pc;
+          }
+        }
+      }
+    } else {
+      for (int w = 0; w < NW && target != 0xFFFFFFFFu; ++w) {
+        uint64_t b = ~rp[w] & valid_mask(w);
+        if (want_safe) b &= ~mp[w];
         const uint32_t pc = (uint32_t)__popcll(b);
         if (target < pc) {
           const int pos = select_bit64(b, target);
           const int r = w * rpw + pos / W;
           act = (int64_t)r * W + (pos - (pos / W) * W);
-          target = 0xFFFFFFFFu;  // found
+          target = 0xFFFFFFFFu;
         } else {
           target -= pc;
         }
@@ -1203,7 +1245,7 @@ __device__ __forceinline__ int tape_cell(uint64_t mine, uint64_t rev, const Geo<
     }
   }
   if (cnt == 0) return 0;
-  const uint32_t target = (uint32_t)(sel % (uint64_t)cnt);
+  const uint32_t target = mod64_small(sel, cnt);
   const uint32_t pc = (uint32_t)__popcll(bits);
   const uint32_t before = wave_excl_scan(pc);
   const bool hit = target >= before && target < before + pc;
@@ -1854,7 +1896,7 @@ int ms_tape_actions(ms_handle* h, uint64_t t, int32_t mode, int64_t* actions, vo
   if (!h || !actions) return fail(MS_EINVAL, "ms_tape_actions: null argument");
   if (mode != MS_TAPE_UNIFORM && mode != MS_TAPE_SAFE_BIASED) return fail(MS_EINVAL, "ms_tape_actions: bad mode");
   const hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((unsigned)((h->n + 255) / 256)), block(256);
+  const dim3 grid((unsigned)((h->n + 63) / 64)), block(64);
   if (h->H == 16 && h->W == 16)
     hipLaunchKernelGGL((k_tape<16, 16>), grid, block, 0, s, h->mine_words, h->rev_words, h->n, h->H, h->W,
                        h->env_begin, t, mode, actions);

@@ -333,7 +333,7 @@ class _HeadsFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, f, pol, mine, *params):
         lp, lm = heads_forward(f, pol, mine)
-        pooled = f.float().mean(1)
+        pooled = f.mean(1, dtype=torch.float32)  # f32 accumulation, no f32 copy of f
         ctx.save_for_backward(f)
         ctx.pol, ctx.mine = pol, mine
         return lp, pooled, lm
@@ -376,4 +376,4 @@ def heads_apply(f: torch.Tensor, pol, mine=None):
     if torch.is_grad_enabled() and (f.requires_grad or any(q.requires_grad for q in params)):
         return _HeadsFn.apply(f, pol, mine, *params)
     lp, lm = heads_forward(f, pol, mine)
-    return lp, f.float().mean(1), lm
+    return lp, f.mean(1, dtype=torch.float32), lm

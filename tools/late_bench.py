@@ -1,0 +1,40 @@
+"""Cost of late-start resets (k_late, one serial wave over the step's done envs in env
+order, as the reference's single shared generator requires) on the tape + step loop.
+
+    python tools/late_bench.py [--envs 4096] [--steps 200]
+"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "minesweeper-ppo_amd"))
+
+import torch  # noqa: E402
+
+from ms_amd import EnvConfig, VecMinesweeper  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--envs", type=int, default=4096)
+ap.add_argument("--steps", type=int, default=200)
+a = ap.parse_args()
+dev = torch.device("cuda:0")
+cfg = EnvConfig(H=16, W=16, mine_count=40)
+for name, late in [("no late start", None),
+                   ("late start p=0.5, 20-120 hidden", dict(prob=0.5, min_hidden=20, max_hidden=120)),
+                   ("late start p=1.0, 20-120 hidden", dict(prob=1.0, min_hidden=20, max_hidden=120))]:
+    v = VecMinesweeper(a.envs, cfg, seed=0, late_start_cfg=late, late_start_seed=1, device=dev)
+    v.reset()
+    dones = 0
+    for t in range(20):
+        v.step(v.tape_actions(t, 0))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for t in range(a.steps):
+        _, _, d, _ = v.step(v.tape_actions(20 + t, 0))
+        dones += d
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / a.steps
+    print(f"{name:34s}: {el * 1e6:7.1f} us/step (eager tape + step), "
+          f"{a.envs / el / 1e6:7.1f} M env-steps/s, {float(dones.sum()) / a.steps:6.1f} resets/step", flush=True)

@@ -69,3 +69,27 @@ def test_fused_model_train_mode_dropout(gpu):
         a, _ = m(obs)
         b, _ = m(obs)
     assert torch.equal(a, b)
+
+
+def test_fused_fp16_overflow_reaches_the_grad_scaler(gpu):
+    """fp16 overflow inside the fused backward (a loss scale far too large) surfaces as
+    non-finite parameter gradients, so GradScaler skips the step and lowers its scale,
+    as with PyTorch's own fp16 autocast path (the reference's ppo.py:25 contract)."""
+    from ms_amd.models import CNNResidualPolicy
+    torch.manual_seed(0)
+    m = CNNResidualPolicy(10, stem_channels=96, blocks=1, dropout=0.0, value_hidden=32).to(gpu)
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-3)
+    obs = _obs(64, 16, 16, gpu)
+    before = {k: p.detach().clone() for k, p in m.named_parameters()}
+    scaler = torch.amp.GradScaler("cuda", init_scale=2.0 ** 60)
+    with torch.autocast("cuda", dtype=torch.float16):
+        assert m.use_fused(obs)
+        lo, v = m(obs)
+        loss = lo.float().square().mean() + v.float().square().mean()
+    scaler.scale(loss).backward()
+    assert not all(torch.isfinite(p.grad).all() for p in m.stem.parameters() if p.grad is not None)
+    scaler.step(opt)
+    scaler.update()
+    assert scaler.get_scale() < 2.0 ** 60
+    for k, p in m.named_parameters():
+        assert torch.equal(p.detach(), before[k]), k  # step skipped

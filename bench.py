@@ -422,9 +422,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # MS_BENCH_BACKEND=gloo with ranks sharing the visible GPUs rehearses the N>1 path
+    # (barriers, max-over-ranks timing, the Trainer's flat-gradient all-reduce) on a
+    # one-GPU box; the driver's multi-GPU runs use the default, RCCL with one GPU per rank.
+    backend = os.environ.get("MS_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local_rank = local_rank % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
 

@@ -727,11 +727,19 @@ __device__ __forceinline__ void board_click(Pcg& rng, uint64_t& mine, uint64_t& 
 // (done, outcome), lane 0 revealed_frac. Reported before the auto-reset (env.py:492-505).
 __device__ __forceinline__ void store_aux(const KParams& p, int64_t idx, int lane, double reward, bool done,
                                           int32_t step_count, uint32_t newly, uint32_t total_rev, int outcome, int A) {
-  uint32_t* d4 = lane == 0 ? reinterpret_cast<uint32_t*>(p.reward)
-                           : (lane == 1 ? reinterpret_cast<uint32_t*>(p.step) : reinterpret_cast<uint32_t*>(p.last_new));
+  // The pointers become scalar values before the per-lane select: selecting between the
+  // fields themselves compiles to a lane-indexed load from the kernel arguments, and its
+  // vmcnt(0) waits for every store in flight (in k_run: the previous step's obs). Global
+  // address space: a generic pointer would become a flat store, which also counts in
+  // lgkmcnt and so holds up the LDS waits behind it.
+  typedef __attribute__((address_space(1))) uint32_t gu32;
+  typedef __attribute__((address_space(1))) uint8_t gu8;
+  const uint64_t pr = rfl64((uint64_t)p.reward), ps = rfl64((uint64_t)p.step), pl = rfl64((uint64_t)p.last_new);
+  const uint64_t pd = rfl64((uint64_t)p.done), po = rfl64((uint64_t)p.outcome);
+  gu32* d4 = (gu32*)(lane == 0 ? pr : (lane == 1 ? ps : pl));
   const uint32_t v4 = lane == 0 ? __float_as_uint((float)reward) : (lane == 1 ? (uint32_t)step_count : newly);
   if (lane < 3 && d4) d4[idx] = v4;
-  uint8_t* d1 = lane == 0 ? p.done : reinterpret_cast<uint8_t*>(p.outcome);
+  gu8* d1 = (gu8*)(lane == 0 ? pd : po);
   const uint8_t v1 = lane == 0 ? (uint8_t)(done ? 1 : 0) : (uint8_t)(int8_t)outcome;
   if (lane < 2 && d1) d1[idx] = v1;
   if (lane == 0 && p.frac) p.frac[idx] = (double)total_rev / (double)(A > 1 ? A : 1);

@@ -856,115 +856,6 @@ __global__ __launch_bounds__(64 * EPW) void k_step(KParams p) {
 }
 
 // ---------------------------------------------------------------------------
-// k_step2: two boards per wave, one after the other. Both boards' inputs are loaded up
-// front; the second board's are forced in (an empty asm use) before the first board's
-// stores issue, so they never queue behind those stores (vmcnt retires in order), and the
-// first board's stores drain while the second board is stepped.
-// ---------------------------------------------------------------------------
-template <int H_, int W_>
-struct StepIn {
-  uint64_t mine, rev;
-  Pcg rng;
-  int32_t step_count;
-  bool fc;
-  int cell;
-};
-
-template <int H_, int W_>
-__device__ __forceinline__ void load_step_in(const KParams& p, int64_t env, const Geo<H_, W_>& g, int lane,
-                                             StepIn<H_, W_>& in) {
-  const int A = g.A(), NW = g.NW();
-  const EnvMeta* mp = p.meta + env;
-  in.mine = load_row(p.mine_words + env * NW, g, lane);
-  in.rev = load_row(p.rev_words + env * NW, g, lane);
-  in.rng.hi = rfl64(mp->st_hi);
-  in.rng.lo = rfl64(mp->st_lo);
-  in.rng.ihi = rfl64(mp->inc_hi);
-  in.rng.ilo = rfl64(mp->inc_lo);
-  in.rng.has32 = rfl(mp->has32);
-  in.rng.uinteger = rfl(mp->uinteger);
-  in.step_count = (int32_t)rfl((uint32_t)mp->step_count);
-  in.fc = (rfl(mp->flags) & 1u) != 0;
-  const uint32_t* ap = reinterpret_cast<const uint32_t*>(p.actions);
-  const int64_t aw = p.actions_i32 ? env : 2 * env;
-  const uint32_t a_lo = ap[aw], a_hi = ap[p.actions_i32 ? aw : aw + 1];
-  int64_t a = p.actions_i32 ? (int64_t)(int32_t)a_lo : (int64_t)(((uint64_t)a_hi << 32) | a_lo);
-  a = (int64_t)rfl64((uint64_t)a);
-  int64_t cell64 = a % A;
-  if (cell64 < 0) cell64 += A;
-  in.cell = (int)cell64;
-}
-
-// the click, then (after `pin`) every store of one board
-template <int H_, int W_, typename Pin>
-__device__ __forceinline__ void step_board(const KParams& p, int64_t env, StepIn<H_, W_>& in, const uint64_t (&J)[4],
-                                           uint64_t* sR, uint64_t* sM, uint32_t* sTab, const Geo<H_, W_>& g,
-                                           int lane, Pin pin) {
-  const int A = g.A(), NW = g.NW();
-  double reward = 0.0;
-  bool done = false;
-  int outcome = MS_OUTCOME_NONE;
-  uint32_t newly = 0, total_rev = 0;
-  bool mines_changed = false;
-  board_click(in.rng, in.mine, in.rev, in.fc, in.cell, p, J, sTab, sR, g, lane, done, outcome, newly, total_rev,
-              mines_changed);
-  pin();
-  if (outcome == MS_OUTCOME_LOSS) reward += p.loss_reward;
-  if (outcome == MS_OUTCOME_WIN) reward += p.win_reward;
-  reward -= p.step_penalty;
-  in.step_count += 1;
-  store_aux(p, env, lane, reward, done, in.step_count, newly, total_rev, outcome, A);
-  if (done) {
-    in.mine = 0ull;
-    in.rev = 0ull;
-    in.fc = false;
-    in.step_count = 0;
-    mines_changed = true;
-  }
-  if (p.obs || p.mask) {
-    stage_rows(sR, sM, in.rev, in.mine, g, lane);
-    emit_obs(p.obs ? p.obs + env * 10 * A : nullptr, p.mask ? p.mask + env * A : nullptr, sR, sM, in.fc, g, lane,
-             reinterpret_cast<uint8_t*>(sTab));
-  }
-  store_meta(p.meta + env, in.rng, in.step_count, in.fc, lane);
-  if (mines_changed) store_rows(p.mine_words + env * NW, in.mine, sR, g, lane);
-  store_rows(p.rev_words + env * NW, in.rev, sR, g, lane);
-  wave_sync();  // the next board re-stages this wave's LDS rows
-}
-
-template <int H_, int W_, int EPW>
-__global__ __launch_bounds__(64 * EPW) void k_step2(KParams p) {
-  __shared__ uint64_t sR_all[EPW][kWave];
-  __shared__ uint64_t sM_all[EPW][kWave + 2];
-  __shared__ uint32_t sTab_all[EPW][(H_ && W_) ? H_ * W_ : kMaxH * kMaxW];
-  const int lane = lane_id();
-  const int wv = (EPW == 1) ? 0 : (int)rfl(threadIdx.x >> 6);
-  const int64_t e0 = ((int64_t)blockIdx.x * EPW + wv) * 2, e1 = e0 + 1;
-  if (e0 >= p.n) return;
-  const bool live1 = e1 < p.n;
-  uint64_t* sR = sR_all[wv];
-  uint64_t* sM = sM_all[wv];
-  uint32_t* sTab = sTab_all[wv];
-  const Geo<H_, W_> g(p.H, p.W);
-  StepIn<H_, W_> b0, b1;
-  load_step_in(p, e0, g, lane, b0);
-  load_step_in(p, live1 ? e1 : e0, g, lane, b1);
-  uint64_t J[4] = {0ull, 0ull, 0ull, 0ull};
-  if (lane < p.K) {
-    const ulonglong2* e = reinterpret_cast<const ulonglong2*>(p.jump + 4 * lane);
-    const ulonglong2 a0 = e[0], a1 = e[1];
-    J[0] = a0.x;
-    J[1] = a0.y;
-    J[2] = a1.x;
-    J[3] = a1.y;
-  }
-  step_board(p, e0, b0, J, sR, sM, sTab, g, lane, [&] {
-    asm volatile("" ::"v"(b1.mine), "v"(b1.rev), "v"(J[0]), "v"(J[1]), "v"(J[2]), "v"(J[3]));
-  });
-  if (live1) step_board(p, e1, b1, J, sR, sM, sTab, g, lane, [] {});
-}
-
-// ---------------------------------------------------------------------------
 // ms_reset: clear boards (RNG continues) + obs zeros + mask ones.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_reset(EnvMeta* meta, uint64_t* mw, uint64_t* rw, int64_t n,
@@ -1663,12 +1554,6 @@ bool shape_ok(const ms_cfg* c) {
 template <int H_, int W_>
 void launch_step(const KParams& p, int epw, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   // generic shapes keep one board per workgroup (their LDS table is sized for 64x62)
-#ifdef MS_STEP2
-  if (H_ && W_ && epw == 4) {
-    hipExtLaunchKernelGGL((k_step2<H_, W_, 4>), dim3((unsigned)((p.n + 7) / 8)), dim3(256), 0, s, ev0, ev1, 0, p);
-    return;
-  }
-#endif
   if (H_ && W_ && epw == 4) {
     hipExtLaunchKernelGGL((k_step<H_, W_, 4>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, ev0, ev1, 0, p);
   } else {

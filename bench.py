@@ -360,12 +360,30 @@ def env_bench(args, world, rank, dev, H, W, K, n_local, multistep=True):
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
-    # Dominant-kernel duration from HIP events on the launch stream: the span of the K-step
-    # graph minus the span of a graph holding only its K tape launches, divided by K = what
-    # one ms_step adds to a step, launch boundary included. (Dispatch-stamped events, used
-    # for k_run, read high on a launch this short: the start stamp is taken while the
-    # preceding k_tape is still running. tools/trace_check.py compares both against the
-    # rocprofv3 trace of the same run.)
+    # Dominant-kernel duration (kernel_ms): the span of a replay of the K-step graph minus
+    # the span of a graph holding only its K tape launches, / K = what one ms_step adds to a
+    # step, launch boundary included. Cross-check (kernel_ms_isolated): Km eager ms_step
+    # launches, each run alone (the host waits for its tape launch first: stamped back to
+    # back, the start stamp would be taken while k_tape still runs) with dispatch-stamped
+    # events (ms_set_timing_events -> hipExtLaunchKernel). Untraced, the isolated figure reads
+    # 1-15 % above the span (each isolated launch starts on an idle GPU); under rocprofv3 both absorb the profiler's per-dispatch overhead on these
+    # ~10-us launches, so tools/trace_check.py's trace fraction is the one to quote there.
+    Km = min(args.steps, 200)
+    timer = DispatchTimer(lib, L, h, Km)
+    t_iso = args.warmup + 2 * args.steps
+    for k in range(Km):
+        t = t_iso + k
+        L.check(lib.ms_tape_actions(h, t, args.tape, ptrs[0], sp))
+        torch.cuda.synchronize()
+        pt = list(ptrs)
+        if not args.diag_no_obs:
+            pt[1], pt[2] = L.ptr(obs_ring[t % R]), L.ptr(mask_ring[t % R])
+        timer.arm(k)
+        L.check(lib.ms_step(h, *pt, sp))
+    timer.disarm()
+    torch.cuda.synchronize()
+    iso_ms = float(np.mean([timer.elapsed_ms(k) for k in range(Km)]))
+    timer.close()
     if graph is not None:
         gt = capture(True)
         ev_full = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -392,9 +410,11 @@ def env_bench(args, world, rank, dev, H, W, K, n_local, multistep=True):
         kern_method = "events around each ms_step (eager)"
     del graph
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kern_ms, iso_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+        elapsed, kern_ms, iso_ms = float(t[0]), float(t[1]), float(t[2])
+    iso_method = (f"dispatch-stamped HIP events (hipExtLaunchKernel) of {Km} eager ms_step launches, "
+                  "each started after its tape launch completed; mean")
 
     traffic, traffic_src = pmc_traffic(H, W, K, n_local)
     bpe = algo_bytes_per_env_step(H, W)
@@ -405,6 +425,7 @@ def env_bench(args, world, rank, dev, H, W, K, n_local, multistep=True):
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                         "kernel": "k_step", "kernel_ms": kern_ms, "kernel_ms_method": kern_method,
+                        "kernel_ms_isolated": iso_ms, "isolated_method": iso_method,
                         "algo_bytes_per_env_step": bpe,
                         "algo_bytes_per_launch": bpe * n_local, "traffic_source": traffic_src}}
     if multistep and not args.diag_no_obs:

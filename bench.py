@@ -59,12 +59,18 @@ def parse():
     ap.add_argument("--board", default="16x16x40")
     ap.add_argument("--tape", type=int, default=0, help="0 uniform-valid, 1 safe-biased")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0,
+                    help="CPU baseline sample budget of the headline point (each extra point: half)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-multistep", action="store_true", help="skip the one-launch ms_run_tape line")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core in os.sched_getaffinity(0)")
-    ap.add_argument("--extras", default="16x16x40:32768,9x9x10:8192,30x16x99:8192",
-                    help="north-star points (board:envs per GPU) measured after the headline; '' disables")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = the CPUs this process may use: min(affinity mask, cgroup quota)")
+    ap.add_argument("--extras", default="16x16x40:32768,9x9x10:8192@total,30x16x99:8192@total",
+                    help="north-star points measured after the headline: board:envs per GPU, or board:envs@total "
+                         "for a GLOBAL env count split over the ranks (C3 / C5 are 8192 envs in all); '' disables")
+    ap.add_argument("--min-timed-steps", type=int, default=1000,
+                    help="the captured K-step graph is replayed until at least this many steps are timed "
+                         "(SURVEY.md §8d: >= 1,000 timed steps)")
     ap.add_argument("--diag-no-obs", action="store_true", help="diagnostic: skip obs/mask outputs")
     ap.add_argument("--graph", type=int, default=1, help="capture the timed steps in a HIP graph")
     ap.add_argument("--ppo-updates", type=int, default=2,
@@ -84,10 +90,34 @@ def _cgroup_cpu_quota():
         return None
 
 
+def effective_cpus():
+    """CPUs this process can actually use: min(affinity mask, cgroup CPU quota)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = _cgroup_cpu_quota()
+    return max(1, min(aff, int(-(-quota // 1)))) if quota else aff
+
+
+# The reference's own env step (env.py VecMinesweeper.step, pure-Python BFS: numba is not in the
+# image), 1 core, measured in the survey container (BASELINE.md:27-32, SURVEY.md §8d). It cannot
+# run on the GPU box (the reference does not travel), so the ratio uses these figures.
+REF_PY_1CORE = {"16x16x40": (6980.0, "16x16x40 N=4096"), "9x9x10": (8338.0, "9x9x10 N=8192"),
+                "16x30x99": (8423.0, "16x30x99 N=1024"),
+                "30x16x99": (8423.0, "16x30x99 N=1024 (the same Expert board, transposed)")}
+
+
+def ref_python_ratio(board, value):
+    ref = REF_PY_1CORE.get(board)
+    if ref is None:
+        return None
+    return {"value": value / ref[0], "ref_env_steps_per_s": ref[0], "ref_config": ref[1],
+            "source": "BASELINE.md:27-32 (reference env.py step, 1 core, Python BFS, survey container)"}
+
+
 def cpu_baseline(H, W, K, n_envs, seed, tape, budget_s, threads):
     """Oracle (CPU restatement of env.py / env_numba, C + pthreads) timed on this host over a
     bounded sample: each thread owns a block of envs and runs tape action + board step for
-    all of them, step after step, without synchronising (one env per task)."""
+    all of them, step after step, without synchronising (one env per task). ``threads`` =
+    the CPUs the process may use (effective_cpus), so ``cores`` is what the sample ran on."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     O.build()
@@ -109,9 +139,9 @@ def cpu_baseline(H, W, K, n_envs, seed, tape, budget_s, threads):
     return dict(value=n_envs * steps / el, unit="env_steps/s", cores=threads, kind="port",
                 nproc=os.cpu_count(), affinity_cpus=len(os.sched_getaffinity(0)), cgroup_cpu_quota=quota,
                 sample=f"{steps} steps x {n_envs} envs {H}x{W}x{K} (tape {tape}) in {el:.1f}s, "
-                       f"oracle/ms_oracle.c mso_run_baseline on {threads} threads (one per core in the "
-                       f"affinity mask; nproc {os.cpu_count()}, cgroup quota "
-                       f"{'none' if quota is None else f'{quota:g} CPUs'})")
+                       f"oracle/ms_oracle.c mso_run_baseline on {threads} threads = min(affinity mask "
+                       f"{len(os.sched_getaffinity(0))}, cgroup quota "
+                       f"{'none' if quota is None else f'{quota:g} CPUs'}); nproc {os.cpu_count()}")
 
 
 class DispatchTimer:
@@ -157,7 +187,8 @@ def multistep_bench(args, world, lib, h, L, n_local, n_total, H, W, bpe, dev):
     # every step writes its own slot (slots=1) of an S-step region holding > 1 GiB, so the
     # stores stream to HBM rather than into the 256 MiB Infinity Cache; K steps = ceil(K/S)
     # launches of S steps (the last one shorter)
-    S = max(1, min(args.steps, -(-(1 << 30) // (n_local * 41 * A))))
+    total = max(args.steps, args.min_timed_steps)
+    S = max(1, min(total, -(-(1 << 30) // (n_local * 41 * A))))
     bufs = [torch.empty((S, n_local, 10, H, W), dtype=torch.float32, device=dev),
             torch.empty((S, n_local, A), dtype=torch.bool, device=dev),
             torch.empty((S, n_local), dtype=torch.float32, device=dev),
@@ -175,13 +206,13 @@ def multistep_bench(args, world, lib, h, L, n_local, n_total, H, W, bpe, dev):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    n_launch = -(-args.steps // S)
+    n_launch = -(-total // S)
     timer = DispatchTimer(lib, L, h, n_launch)
     t0 = time.perf_counter()
     done_steps = 0
     i = 0
-    while done_steps < args.steps:
-        T = min(S, args.steps - done_steps)
+    while done_steps < total:
+        T = min(S, total - done_steps)
         timer.arm(i)
         L.check(lib.ms_run_tape(h, t_base + S + done_steps, T, args.tape, 1, None, *ptrs, sp))
         done_steps += T
@@ -190,7 +221,7 @@ def multistep_bench(args, world, lib, h, L, n_local, n_total, H, W, bpe, dev):
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    kern_ms = sum(timer.elapsed_ms(j) for j in range(n_launch)) / args.steps
+    kern_ms = sum(timer.elapsed_ms(j) for j in range(n_launch)) / total
     timer.close()
     if world > 1:
         t = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
@@ -199,7 +230,8 @@ def multistep_bench(args, world, lib, h, L, n_local, n_total, H, W, bpe, dev):
     achieved = bpe * n_local / (kern_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(H, W, args.board_k, n_local, "k_run")
     return {"metric": "env steps/sec, S synthetic-policy steps per launch (ms_run_tape)",
-            "value": n_total * args.steps / el, "unit": "env_steps/s", "ms_per_step": el / args.steps * 1e3,
+            "value": n_total * total / el, "unit": "env_steps/s", "ms_per_step": el / total * 1e3,
+            "timed_steps": total,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes per step",
                          "traffic_source": traffic_src, "kernel": "k_run",
@@ -265,6 +297,27 @@ def ppo_bench(args, world, rank, local_rank, dev):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t[0])
     spu = el / args.ppo_updates
+    n_mb = cfg.ppo_epochs * cfg.mini_batches
+    comm = {"allreduce": None, "note": "world 1: no collective"}
+    if world > 1:
+        # the per-minibatch RCCL all-reduce of the flat fp32 gradient bucket (FlatGrads), timed
+        # alone: barrier, 5 warm-up calls, then 20 calls between two synchronisations; max over ranks
+        flat = tr.flat
+        for _ in range(5):
+            flat.all_reduce_mean(info.group)
+        torch.cuda.synchronize()
+        dist.barrier()
+        ta = time.perf_counter()
+        for _ in range(20):
+            flat.all_reduce_mean(info.group)
+        torch.cuda.synchronize()
+        ar_s = (time.perf_counter() - ta) / 20
+        t = torch.tensor([ar_s], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ar_s = float(t[0])
+        comm = {"allreduce_ms_per_minibatch": ar_s * 1e3, "bytes": flat.flat.numel() * 4,
+                "allreduces_per_update": n_mb, "bus_GBps": 2 * (world - 1) / world * flat.flat.numel() * 4 / ar_s / 1e9,
+                "share_of_update": n_mb * ar_s / spu, "backend": dist.get_backend()}
     n_loc, T = args.envs, cfg.steps_per_env
     gflop = (T * n_loc * GFLOP_FWD_16 + n_loc * GFLOP_FWD_16 + cfg.ppo_epochs * T * n_loc * GFLOP_FWDBWD_16)
     mean = lambda k: float(np.mean([p[k] for p in prof]))  # noqa: E731
@@ -280,7 +333,7 @@ def ppo_bench(args, world, rank, local_rank, dev):
                          "traffic": kprof[dom]["traffic_bytes_per_launch"] if dom else None,
                          "traffic_kernel": dom, "traffic_unit": "HBM bytes per launch at N=32768",
                          "algo_gflop_per_update_per_gpu": gflop, "trunk_kernels": kprof},
-            "loss": prof[-1].get("loss"), "entropy": prof[-1].get("entropy")}
+            "comm": comm, "loss": prof[-1].get("loss"), "entropy": prof[-1].get("entropy")}
 
 
 def env_bench(args, world, rank, dev, H, W, K, n_local, multistep=True):
@@ -346,15 +399,20 @@ def env_bench(args, world, rank, dev, H, W, K, n_local, multistep=True):
         return g  # capture does not execute: the board state is still at step `warmup`
 
     graph = capture(False) if args.graph else None
+    # the K-step graph is replayed back to back until >= min_timed_steps steps are timed, so a
+    # short --steps does not leave the one host-side graph launch as a visible share of the span
+    reps = max(1, -(-args.min_timed_steps // args.steps))
+    timed = args.steps * reps
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     if graph is not None:
-        graph.replay()
+        for _ in range(reps):
+            graph.replay()
     else:
-        for k in range(args.steps):
-            one_step(args.warmup + k, sp)
+        for k in range(timed):
+            one_step(args.warmup + k % args.steps, sp)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -368,7 +426,7 @@ def env_bench(args, world, rank, dev, H, W, K, n_local, multistep=True):
     # events (ms_set_timing_events -> hipExtLaunchKernel). Untraced, the isolated figure reads
     # 1-15 % above the span (each isolated launch starts on an idle GPU); under rocprofv3 both absorb the profiler's per-dispatch overhead on these
     # ~10-us launches, so tools/trace_check.py's trace fraction is the one to quote there.
-    Km = min(args.steps, 200)
+    Km = min(timed, 200)
     timer = DispatchTimer(lib, L, h, Km)
     t_iso = args.warmup + 2 * args.steps
     for k in range(Km):
@@ -391,14 +449,16 @@ def env_bench(args, world, rank, dev, H, W, K, n_local, multistep=True):
         # the step graph is replayed once more for the span: the boards move on, the work per
         # step is statistically the same
         ev_full[0].record()
-        graph.replay()
+        for _ in range(reps):
+            graph.replay()
         ev_full[1].record()
         ev_tape[0].record()
-        gt.replay()
+        for _ in range(reps):
+            gt.replay()
         ev_tape[1].record()
         torch.cuda.synchronize()
-        kern_ms = (ev_full[0].elapsed_time(ev_full[1]) - ev_tape[0].elapsed_time(ev_tape[1])) / args.steps
-        kern_method = "graph span difference (tape+step vs tape only) / K"
+        kern_ms = (ev_full[0].elapsed_time(ev_full[1]) - ev_tape[0].elapsed_time(ev_tape[1])) / timed
+        kern_method = "graph span difference (tape+step vs tape only, each K-step graph replayed R times) / (K*R)"
         del gt
     else:
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -420,8 +480,9 @@ def env_bench(args, world, rank, dev, H, W, K, n_local, multistep=True):
     bpe = algo_bytes_per_env_step(H, W)
     achieved = bpe * n_local / (kern_ms * 1e-3) / 1e9
     res = {"board": f"{H}x{W}x{K}", "envs_per_gpu": n_local, "envs_total": n_total,
-           "value": n_total * args.steps / elapsed, "unit": "env_steps/s",
-           "ms_per_step": elapsed / args.steps * 1e3, "obs_ring_slots": R,
+           "value": n_total * timed / elapsed, "unit": "env_steps/s",
+           "ms_per_step": elapsed / timed * 1e3, "timed_steps": timed, "graph_replays": reps,
+           "obs_ring_slots": R,
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                         "kernel": "k_step", "kernel_ms": kern_ms, "kernel_ms_method": kern_method,
@@ -460,6 +521,17 @@ def main():
 
     n_local = args.envs
     head = env_bench(args, world, rank, dev, H, W, K, n_local, multistep=not args.no_multistep)
+    cpu_on = rank == 0 and world == 1 and not args.no_cpu_baseline
+    threads = args.cpu_threads or effective_cpus()
+
+    def add_cpu(point, h_, w_, k_, n_, budget):
+        """cpu_baseline + ratios of one measured point (rank 0, N=1 only)."""
+        if not cpu_on:
+            return
+        cb = cpu_baseline(h_, w_, k_, n_, args.seed, args.tape, budget, threads)
+        point["cpu_baseline"] = cb
+        point["gpu_over_cpu"] = point["value"] / cb["value"]
+        point["gpu_over_ref_python_1core"] = ref_python_ratio(f"{h_}x{w_}x{k_}", point["value"])
     out = {
         "metric": "env steps/sec (16x16x40, N envs) + PPO updates/sec at 1/2/4/8 MI355X",
         "value": head["value"],
@@ -467,6 +539,8 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "timed_steps": head["timed_steps"],
+        "graph_replays": head["graph_replays"],
         "ms_per_step": head["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
@@ -482,22 +556,29 @@ def main():
     }
     if "multistep" in head:
         out["multistep"] = head["multistep"]
+    pts = []
     if args.extras and not args.diag_no_obs:
-        pts = []
         for item in args.extras.split(","):
             b, n = item.split(":")
             h_, w_, k_ = (int(x) for x in b.lower().split("x"))
-            r = env_bench(args, world, rank, dev, h_, w_, k_, int(n), multistep=not args.no_multistep)
-            pts.append(r)
-        out["north_star_points"] = pts
+            if n.endswith("@total"):  # a GLOBAL env count, split over the ranks
+                n_tot = int(n[:-len("@total")])
+                if n_tot % world:
+                    raise SystemExit(f"--extras {item}: {n_tot} envs do not split over {world} ranks")
+                n_pg = n_tot // world
+            else:
+                n_pg = int(n)
+            r = env_bench(args, world, rank, dev, h_, w_, k_, n_pg, multistep=not args.no_multistep)
+            pts.append((r, h_, w_, k_, n_pg))
+        out["north_star_points"] = [r for r, *_ in pts]
     if args.ppo_updates > 0:
         out["ppo"] = ppo_bench(args, world, rank, local_rank, dev)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = args.cpu_threads or len(os.sched_getaffinity(0))
-        out["cpu_baseline"] = cpu_baseline(H, W, K, n_local, args.seed, args.tape, args.cpu_seconds,
-                                           threads)
-        out["gpu_over_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+    # CPU baselines last, after every GPU measurement: rank 0 at N=1, a bounded sample per point
+    add_cpu(out, H, W, K, n_local, args.cpu_seconds)
+    if cpu_on:
         out["gpu_over_cpu_target"] = 50.0
+    for r, h_, w_, k_, n_pg in pts:
+        add_cpu(r, h_, w_, k_, n_pg, args.cpu_seconds / 2)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

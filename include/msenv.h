@@ -175,6 +175,17 @@ int ms_sample_masked(const float* logits, const uint8_t* mask, int64_t N,
                      uint64_t counter, int64_t* actions, float* logp,
                      void* stream);
 
+/* Replaces nn.Dropout2d's torch-RNG channel masks in the training forward
+ * (cnn_residual.py:14,22; train mode in collect_rollout train_rl.py:221 and in
+ * ppo_update ppo.py:25-30). rows int64[N] = GLOBAL sample ids (buffer row
+ * t*num_envs_total + global env). Writes out f32[nblk][N][C] = keep / (1-p),
+ * keep = u(seed, counter, rows[i], b*C + c) >= p from a counter-based hash, so
+ * a data-parallel rank draws exactly the masks its samples get in a one-GPU
+ * run. C % 4 == 0, 0 < p < 1. */
+int ms_dropout_masks(const int64_t* rows, int64_t N, int32_t nblk, int32_t C,
+                     uint64_t seed, uint64_t counter, float p, float* out,
+                     void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1376,6 +1376,36 @@ __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t counter, uint
   return ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
 }
 
+// ---------------------------------------------------------------------------
+// ms_dropout_masks: Dropout2d channel masks keyed by GLOBAL sample index.
+// out[b][i][c] = (u(seed', counter, rows[i], b*C + c) >= p) / (1 - p), so a
+// sample draws the same masks whichever rank (or minibatch position) holds it.
+// One thread per 4 output channels (float4 store).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_dropout(const int64_t* __restrict__ rows, int64_t N, int nblk, int C,
+                                                 uint64_t seed, uint64_t counter, float p, float scale,
+                                                 float* __restrict__ out) {
+  const int C4 = C >> 2;
+  const int64_t total = (int64_t)nblk * N * C4;
+  const uint64_t s = splitmix64(seed ^ 0xD1B54A32D192ED03ull);  // domain-separated from k_sample
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int c4 = (int)(q % C4);
+    const int64_t bi = q / C4;
+    const int64_t i = bi % N;
+    const int b = (int)(bi / N);
+    const uint64_t row = (uint64_t)rows[i];
+    float4 v;
+    float* vp = &v.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float u = uniform01(s, counter, row, (uint64_t)(b * C + 4 * c4 + j));
+      vp[j] = u >= p ? scale : 0.f;
+    }
+    reinterpret_cast<float4*>(out)[q] = v;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_sample(const float* __restrict__ logits, const uint8_t* __restrict__ mask,
                                                 int64_t N, int A, int64_t row_begin, uint64_t seed,
                                                 uint64_t counter, int64_t* __restrict__ actions,
@@ -1942,6 +1972,18 @@ int ms_sample_masked(const float* logits, const uint8_t* mask, int64_t N, int32_
                      (int)A, row_begin, seed, counter, actions, logp);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? MS_OK : hip_fail(e, "ms_sample_masked launch");
+}
+
+int ms_dropout_masks(const int64_t* rows, int64_t N, int32_t nblk, int32_t C, uint64_t seed, uint64_t counter,
+                     float p, float* out, void* stream) {
+  if (!rows || !out || N <= 0 || nblk <= 0 || C <= 0 || (C & 3) || !(p > 0.f && p < 1.f))
+    return fail(MS_EINVAL, "ms_dropout_masks: bad argument");
+  const int64_t total = (int64_t)nblk * N * (C / 4);
+  const unsigned grid = (unsigned)std::min<int64_t>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_dropout, dim3(grid), dim3(256), 0, (hipStream_t)stream, rows, N, (int)nblk, (int)C, seed,
+                     counter, p, 1.0f / (1.0f - p), out);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? MS_OK : hip_fail(e, "ms_dropout_masks launch");
 }
 
 }  // extern "C"

@@ -5,15 +5,24 @@ board step (HIP, libmsenv.so), on-device rollout storage + GAE, the residual
 CNN policy under PyTorch-ROCm, and the PPO update with an RCCL gradient
 all-reduce across ranks.
 """
+import logging as _logging
 import os as _os
-
-# fp32 means fp32: MIOpen's Winograd solvers for fp32 3x3 convolutions give gradients of the
-# shipped model ~130x further from a float64 computation than the reference's own fp32 CPU
-# gradients (tools/grad_diag.py on MI355X); without them the error is <= 2x (DESIGN.md §5).
-# The bf16 training path runs the fused kernels and never reaches MIOpen. Must be set before
-# MIOpen's first convolution; an explicit user setting wins.
-_os.environ.setdefault("MIOPEN_DEBUG_CONV_WINOGRAD", "0")
 
 from .env import EnvConfig, VecMinesweeper, OBS_CHANNELS  # noqa: F401
 
-__all__ = ["EnvConfig", "VecMinesweeper", "OBS_CHANNELS"]
+
+def exact_fp32_convs() -> bool:
+    """fp32 means fp32: MIOpen's Winograd solvers for fp32 3x3 convolutions give gradients of the
+    shipped model ~130x further from a float64 computation than the reference's own fp32 CPU
+    gradients (tools/grad_diag.py on MI355X); without them the error is <= 2x.
+    Sets MIOPEN_DEBUG_CONV_WINOGRAD=0 unless the user chose a value, and logs it once. MIOpen
+    reads it at its first convolution, so entry points (train / eval main, the tests) call this
+    before any model runs. The 16-bit training path runs the fused kernels and never reaches
+    MIOpen. Returns True when the setting is in effect."""
+    if "MIOPEN_DEBUG_CONV_WINOGRAD" not in _os.environ:
+        _os.environ["MIOPEN_DEBUG_CONV_WINOGRAD"] = "0"
+        _logging.getLogger("ms_amd").info("MIOPEN_DEBUG_CONV_WINOGRAD=0 (exact fp32 convolutions)")
+    return _os.environ["MIOPEN_DEBUG_CONV_WINOGRAD"] == "0"
+
+
+__all__ = ["EnvConfig", "VecMinesweeper", "OBS_CHANNELS", "exact_fp32_convs"]

@@ -53,7 +53,8 @@ SIGNATURES = {
     "ms_run_tape": [_vp, _u64, _i32, _i32, _i32] + [_vp] * 10,
     "ms_gae": [_vp, _vp, _vp, _vp, _i32, _i64, _f32, _f32, _vp, _vp, _vp],
     "ms_sample_masked": [_vp, _vp, _i64, _i32, _i64, _u64, _u64, _vp, _vp, _vp],
-    "ms_set_late_start": [_vp, ctypes.c_double, _i32, _i32, _i32, _i32, _u64],
+    "ms_dropout_masks": [_vp, _i64, _i32, _i32, _u64, _u64, _f32, _vp, _vp],
+    "ms_set_late_start":[_vp, ctypes.c_double, _i32, _i32, _i32, _i32, _u64],
     "ms_late_rng_state": [_vp, _vp],
     # msenv_debug.h
     "ms_set_debug_flags": [_vp, ctypes.c_uint32],

@@ -56,6 +56,10 @@ class RolloutBuffer:
             self.mine_labels = torch.zeros((B, H, W), dtype=torch.float32, device=device)
             self.mine_valid = torch.zeros((B, H, W), dtype=torch.bool, device=device)
         self._t = 0
+        # this buffer's envs within the global env list (set by collect_rollout for a shard):
+        # buffer row t*num_envs + e is global sample t*num_envs_total + env_begin + e
+        self.env_begin = 0
+        self.num_envs_total = num_envs
 
     # --------------------------------------------------------------- writes
     def slot(self, t: int) -> Dict[str, torch.Tensor]:
@@ -142,10 +146,15 @@ class RolloutBuffer:
         for s in range(0, rows_s, m_s):
             yield self._gather(P[:, s:s + m_s].reshape(-1))
 
+    def global_rows(self, sel: torch.Tensor) -> torch.Tensor:
+        """Buffer rows -> global sample ids t * num_envs_total + env_begin + e."""
+        return (sel // self.num_envs) * self.num_envs_total + self.env_begin + sel % self.num_envs
+
     def _gather(self, sel: torch.Tensor) -> Batch:
         kw = dict(obs=self.obs[sel], action_mask=self.action_mask[sel], actions=self.actions[sel],
                   old_logp=self.logp[sel], rewards=self.rewards[sel], dones=self.dones[sel],
-                  values=self.values[sel], advantages=self.advantages[sel], returns=self.returns[sel])
+                  values=self.values[sel], advantages=self.advantages[sel], returns=self.returns[sel],
+                  rows=self.global_rows(sel))
         if self.mine_labels is not None:
             kw["mine_labels"] = self.mine_labels[sel]
             if self.mine_valid is not None:

@@ -211,6 +211,8 @@ def main(argv=None) -> None:
     ap.add_argument("--debug_eval", action="store_true", help="accepted; not implemented on device")
     ap.add_argument("--amp", choices=["fp32", "bf16", "fp16"], default="fp32")
     args = ap.parse_args(argv)
+    from . import exact_fp32_convs
+    exact_fp32_convs()
     device = torch.device("cuda")
     if args.ckpt:
         ckpt = args.ckpt

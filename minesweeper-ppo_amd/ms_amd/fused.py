@@ -254,19 +254,21 @@ def trunk_params(layers) -> list:
     return [p for conv, norm in layers for p in (conv.weight, conv.bias, norm.weight, norm.bias)]
 
 
-def fused_features(model, obs: torch.Tensor, dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
+def fused_features(model, obs: torch.Tensor, dtype: torch.dtype = torch.bfloat16,
+                   dmasks: Optional[list] = None) -> torch.Tensor:
     """Trunk features of CNNResidualPolicy as NHWC ``dtype`` [N, H*W, 96] via the fused kernels
-    (``dtype``: the autocast type, bf16 or fp16). Dropout2d masks are drawn here (torch RNG)
-    when the model is in training mode."""
+    (``dtype``: the autocast type, bf16 or fp16). ``dmasks``: per-block Dropout2d masks [N, 96]
+    (keep / (1 - p), ms_amd.dropout); without them a training-mode model draws torch-RNG masks."""
     n, c, H, W = obs.shape
     layers = trunk_layers(model)
     x0 = obs_to_nhwc(obs, 16, dtype)
     nblk = len(model.residual_stack)
-    p = model.residual_stack[0].dropout.p if isinstance(model.residual_stack[0].dropout, torch.nn.Dropout2d) else 0.0
-    dmasks = None
-    if model.training and p > 0:
+    p = model.dropout_p()
+    if dmasks is None and model.training and p > 0:
         keep = torch.rand(nblk, n, COUT, device=obs.device) >= p
         dmasks = [(keep[i].float() * (1.0 / (1.0 - p))).contiguous() for i in range(nblk)]
+    elif not (model.training and p > 0):
+        dmasks = None
     params = trunk_params(layers)
     if torch.is_grad_enabled() and any(q.requires_grad for q in params):
         return _TrunkFn.apply(x0, H, W, dmasks, layers, *params)

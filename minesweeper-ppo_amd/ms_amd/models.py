@@ -9,13 +9,16 @@ creation order are the reference's, so (a) checkpoints load unchanged
 (b) ``torch.manual_seed(s)`` yields bit-identical initial weights (checked
 against tests/golden/model_full_*.npz).
 
-MI355X notes: the 3x3 conv stack runs as MIOpen implicit-GEMM convolutions on
-MFMA under bf16 autocast; ``channels_last()`` switches the
-activations to NHWC, which MIOpen's MFMA conv kernels prefer.
+MI355X notes: on a HIP device under bf16 or fp16 autocast with the shipped trunk
+width (96), the residual trunk and the policy / belief heads run as hand-written
+MFMA kernels (csrc/mscnn*.hip, csrc/msheads.hip via ms_amd.fused).
+Every other case (fp32, CPU, other widths) runs the PyTorch op chain below;
+``model.fused = False`` forces that chain. Dropout2d masks come from the keyed
+hash of ms_amd.dropout when a key is set (the Trainer sets one per forward), so a
+data-parallel rank draws the masks its samples get in a one-GPU run.
 """
 from __future__ import annotations
 
-import os
 from typing import Dict, Optional
 
 import torch
@@ -65,8 +68,10 @@ class _ResidualBlock(nn.Module):
         self.dropout = nn.Dropout2d(dropout) if dropout > 0 else nn.Identity()
         self.act = nn.ReLU(inplace=True)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        y = self.dropout(self.act(self.norm1(self.conv1(x))))
+    def forward(self, x: torch.Tensor, dmask: Optional[torch.Tensor] = None) -> torch.Tensor:
+        y = self.act(self.norm1(self.conv1(x)))
+        # dmask: keyed Dropout2d mask [N, C] (keep / (1 - p)), in place of the torch-RNG draw
+        y = y * dmask.to(y.dtype)[:, :, None, None] if dmask is not None else self.dropout(y)
         y = self.norm2(self.conv2(y))
         return self.act(y + x)
 
@@ -95,9 +100,10 @@ class CNNResidualPolicy(nn.Module):
         )
         self.mine_head = _pointwise_head(C)
 
-        # fused MFMA trunk (csrc/mscnn*.hip) on HIP devices under bf16 or fp16 autocast;
-        # MS_AMD_FUSED=0 forces the PyTorch op chain (A/B measurements)
-        self.fused = os.environ.get("MS_AMD_FUSED", "1") != "0"
+        # fused MFMA trunk + heads (csrc/mscnn*.hip, csrc/msheads.hip) on HIP devices under
+        # bf16 or fp16 autocast; False forces the PyTorch op chain
+        self.fused = True
+        self._dropout_key = None  # (global sample ids, seed, counter): ms_amd.dropout.keyed_dropout
 
     def set_gradient_checkpointing(self, enabled: bool) -> None:  # API parity (no-op, as the reference)
         return None
@@ -108,24 +114,29 @@ class CNNResidualPolicy(nn.Module):
                 and x.shape[2] * x.shape[3] <= 512 and torch.is_autocast_enabled("cuda")
                 and torch.get_autocast_dtype("cuda") in (torch.bfloat16, torch.float16))
 
-    def features(self, x: torch.Tensor) -> torch.Tensor:
-        return self.residual_stack(self.stem(x))
+    def dropout_p(self) -> float:
+        d = self.residual_stack[0].dropout
+        return float(d.p) if isinstance(d, nn.Dropout2d) else 0.0
 
-    def _heads_nhwc(self, f: torch.Tensor, H: int, W: int, return_mine: bool):
-        """The three heads on NHWC trunk features [N, H*W, C]: a 1x1 conv is a linear map
-        over channels, so policy/mine heads are two GEMMs over N*H*W rows."""
-        def pointwise(head, t):
-            c0, c2 = head[0], head[2]
-            h = F.relu(F.linear(t, c0.weight.flatten(1), c0.bias))
-            return F.linear(h, c2.weight.flatten(1), c2.bias).squeeze(-1)
-        n = f.shape[0]
-        logits = pointwise(self.policy_head, f)  # [N, H*W], index r*W + c
-        vh = self.value_head
-        v = f.float().mean(1)  # AdaptiveAvgPool2d(1) + Flatten
-        value = vh[6](F.relu(vh[4](F.relu(vh[2](v))))).squeeze(-1)
-        if return_mine:
-            return logits, value, pointwise(self.mine_head, f.detach()).view(n, 1, H, W)
-        return logits, value
+    def keyed_masks(self, n: int) -> Optional[list]:
+        """Per-block Dropout2d masks [N, C] from the keyed hash, when a key is set, the model
+        is training and dropout is on; None otherwise (torch-RNG Dropout2d applies)."""
+        key = self._dropout_key
+        p = self.dropout_p()
+        if key is None or not self.training or p <= 0:
+            return None
+        rows, seed, counter = key
+        if rows.shape[0] != n:
+            raise ValueError(f"dropout key holds {rows.shape[0]} sample ids for a batch of {n}")
+        from .dropout import dropout_masks
+        m = dropout_masks(rows, len(self.residual_stack), self.stem[0].out_channels, p, seed, counter)
+        return list(m.unbind(0))
+
+    def features(self, x: torch.Tensor, dmasks: Optional[list] = None) -> torch.Tensor:
+        f = self.stem(x)
+        for i, blk in enumerate(self.residual_stack):
+            f = blk(f, dmasks[i] if dmasks is not None else None)
+        return f
 
     def _heads_fused(self, f: torch.Tensor, H: int, W: int, return_mine: bool):
         """Heads through csrc/msheads.hip: policy + mine logits and the pooled features in
@@ -139,11 +150,12 @@ class CNNResidualPolicy(nn.Module):
         return logits, value
 
     def forward(self, x: torch.Tensor, return_mine: bool = False):
+        dmasks = self.keyed_masks(x.shape[0])
         if self.use_fused(x):
             from .fused import fused_features
-            f = fused_features(self, x, torch.get_autocast_dtype("cuda"))
+            f = fused_features(self, x, torch.get_autocast_dtype("cuda"), dmasks=dmasks)
             return self._heads_fused(f, x.shape[2], x.shape[3], return_mine)
-        f = self.features(x)
+        f = self.features(x, dmasks)
         n = f.shape[0]
         # [N,1,H,W] -> [N,H*W], index r*W + c (cnn_residual.py:89)
         logits = self.policy_head(f).reshape(n, -1)

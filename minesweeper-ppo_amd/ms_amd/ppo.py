@@ -16,6 +16,7 @@ Gradients are averaged with ONE all-reduce over a flat bucket (FlatGrads).
 """
 from __future__ import annotations
 
+import weakref
 from contextlib import nullcontext
 from dataclasses import dataclass
 from typing import Dict, Optional
@@ -54,12 +55,21 @@ class FlatGrads:
         dev = self.params[0].device
         self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
         self.reached = set()
-        for p in self.params:
-            p.register_post_accumulate_grad_hook(self._mark)
+        # the hooks hold only a weak reference: a dropped FlatGrads (and its flat buffer) is
+        # freed, and its hooks are removed by the finaliser or by close()
+        ref = weakref.ref(self)
+
+        def mark(p, ref=ref):
+            me = ref()
+            if me is not None:
+                me.reached.add(id(p))
+        self._handles = [p.register_post_accumulate_grad_hook(mark) for p in self.params]
+        self._finalizer = weakref.finalize(self, _remove_hooks, self._handles)
         self.attach()
 
-    def _mark(self, p):
-        self.reached.add(id(p))
+    def close(self):
+        """Remove the hooks (the gradients stay as they are)."""
+        self._finalizer()
 
     def attach(self):
         o = 0
@@ -89,6 +99,12 @@ class FlatGrads:
     def all_reduce_mean(self, group=None):
         dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
         self.flat.div_(dist.get_world_size(group))
+
+
+def _remove_hooks(handles):
+    for h in handles:
+        h.remove()
+    handles.clear()
 
 
 def _autocast(batch_obs: torch.Tensor, amp_dtype: Optional[torch.dtype]):
@@ -155,7 +171,10 @@ def ppo_update(model, optimizer, batch, cfg: PPOConfig, scaler=None, *,
                flat_grads: Optional[FlatGrads] = None, sync_stats: bool = True):
     """One minibatch update (ppo.py:23-119). With ``sync_stats=False`` the
     stats stay on device (0-dim tensors) so a caller can average them over an
-    update with a single host sync."""
+    update with a single host sync. A data-parallel call (``group``) needs
+    ``flat_grads``: the gradient all-reduce runs over its flat bucket."""
+    if group is not None and flat_grads is None:
+        raise ValueError("ppo_update(group=...) needs flat_grads=FlatGrads(model.parameters())")
     out = ppo_losses(model, batch, cfg, amp_dtype=amp_dtype, group=group)
     loss = out["loss"]
     if flat_grads is not None:

@@ -13,7 +13,8 @@ action distribution equals softmax(masked logits) (checked statistically in
 tests); the stream of random numbers is not torch's, hence rollouts are not
 bitwise those of torch.distributions.Categorical. The hash is keyed by the
 GLOBAL env index, so a rank's shard draws what the same envs draw in an
-unsharded run: rollouts do not depend on the world size.
+unsharded run: rollouts do not depend on the world size. The training-mode
+forward's Dropout2d masks are keyed the same way (ms_amd.dropout).
 """
 from __future__ import annotations
 
@@ -25,6 +26,7 @@ import torch
 
 from . import _lib as L
 from .buffers import RolloutBuffer
+from .dropout import ROLLOUT, keyed_dropout, mix_seed
 from .env import OBS_CHANNELS, VecMinesweeper
 
 
@@ -66,6 +68,10 @@ def collect_rollout(vec: VecMinesweeper, model: torch.nn.Module, steps: int, dev
     if buffer is None or buffer.num_envs != N or buffer.steps != steps or \
             (need_aux and buffer.mine_labels is None):
         buffer = RolloutBuffer(N, steps, (OBS_CHANNELS, H, W), H * W, device, with_mine_labels=need_aux)
+    # global sample ids (row t * num_envs_total + global env): keys of the Dropout2d masks
+    buffer.env_begin, buffer.num_envs_total = vec.env_begin, vec.num_envs_total
+    env_ids = torch.arange(vec.env_begin, vec.env_begin + N, dtype=torch.int64, device=device)
+    dseed = mix_seed(sample_seed, ROLLOUT)
     t0 = time.perf_counter()
     s0 = buffer.slot(0)
     vec.reset(out={"obs": s0["obs"], "action_mask": s0["action_mask"]})
@@ -75,7 +81,8 @@ def collect_rollout(vec: VecMinesweeper, model: torch.nn.Module, steps: int, dev
         s = buffer.slot(t)
         if need_aux:
             vec.mine_labels(s["mine_labels"], s["mine_valid"])
-        with _autocast(device, amp_dtype):
+        with _autocast(device, amp_dtype), \
+                keyed_dropout(model, env_ids + t * vec.num_envs_total, dseed, sample_counter + t):
             logits, values = model(s["obs"])
         sample_masked(logits, s["action_mask"], sample_seed, sample_counter + t, s["actions"], s["logp"],
                       row_begin=vec.env_begin)
@@ -87,7 +94,8 @@ def collect_rollout(vec: VecMinesweeper, model: torch.nn.Module, steps: int, dev
             out = {"obs": last_obs, "action_mask": last_mask}
         out["rewards"], out["dones"] = s["rewards"], s["dones"]
         vec.step(s["actions"], out=out)
-    with _autocast(device, amp_dtype):
+    with _autocast(device, amp_dtype), \
+            keyed_dropout(model, env_ids + steps * vec.num_envs_total, dseed, sample_counter + steps):
         _, last_values = model(last_obs)
     last_values = last_values.float()
     buffer._t = steps

@@ -32,6 +32,7 @@ from torch.optim.lr_scheduler import CosineAnnealingLR
 
 from .buffers import RolloutBuffer
 from .dist import DistInfo, broadcast_module, init_from_env
+from .dropout import MINIBATCH, keyed_dropout, mix_seed
 from .env import EnvConfig, VecMinesweeper
 from .models import build_model, strip_compile_prefix
 from .ppo import FlatGrads, PPOConfig, ppo_update
@@ -153,6 +154,10 @@ class Trainer:
             cfg.num_envs = int(rollout["num_envs"])
         if "steps_per_env" in rollout:
             cfg.steps_per_env = int(rollout["steps_per_env"])
+        if cfg.num_envs % self.info.world:
+            # equal shards are what make every rank run the same number of minibatches (each
+            # one ends in collectives) and the mean of the rank means the global mean
+            raise ValueError(f"num_envs={cfg.num_envs} must be a multiple of the world size {self.info.world}")
         env_kwargs = {"H": cfg.H, "W": cfg.W, "mine_count": cfg.mine_count,
                       "guarantee_safe_neighborhood": cfg.guarantee_safe_neighborhood}
         env_kwargs.update(env_d)
@@ -187,9 +192,14 @@ class Trainer:
         # minibatches are stratified over S stripes of the global env list (RolloutBuffer.
         # get_stratified_minibatches): with S a multiple of the world size, rank r's minibatch k
         # is its part of the unsharded run's minibatch k, so training does not depend on world
+        # (minibatch_strata: 1 at world 1 is the reference's single randperm over the buffer).
+        # A requested S that does not divide num_envs or is not a multiple of the world size
+        # falls back to S = world, which divides num_envs (checked above): every rank then
+        # holds num_envs / S envs per stripe and the same number of rows and minibatches.
         S = int(training.get("minibatch_strata", 8))
         if S <= 0 or cfg.num_envs % S or S % self.info.world:
             S = self.info.world
+        assert cfg.num_envs % S == 0 and S % self.info.world == 0
         self.strata = S
         self.stripes_local = S // self.info.world
         self.stripe_begin = self.info.rank * self.stripes_local
@@ -218,12 +228,15 @@ class Trainer:
         acc: Dict[str, torch.Tensor] = {}
         n = 0
         group = self.info.group if self.info.world > 1 else None
+        dseed = mix_seed(self.seed * 7919 + 17, MINIBATCH)
         for epoch in range(cfg.ppo_epochs):
             mbs = self.buffer.get_stratified_minibatches(cfg.mini_batches, self.stripes_local, self.stripe_begin,
                                                          seed=(self.seed * 1000003 + update) * 64 + epoch)
-            for batch in mbs:
-                st = ppo_update(self.model, self.opt, batch, pc, self.scaler, amp_dtype=self.amp_dtype,
-                                group=group, flat_grads=self.flat, sync_stats=False)
+            for k, batch in enumerate(mbs):
+                # Dropout2d masks keyed by (update, epoch, minibatch, global sample id)
+                with keyed_dropout(self.model, batch.rows, dseed, (((update << 8) + epoch) << 16) + k):
+                    st = ppo_update(self.model, self.opt, batch, pc, self.scaler, amp_dtype=self.amp_dtype,
+                                    group=group, flat_grads=self.flat, sync_stats=False)
                 for k, v in st.items():
                     acc[k] = acc[k] + v if k in acc else v
                 n += 1
@@ -308,6 +321,8 @@ def main(argv=None) -> None:
     ap.add_argument("--grad_checkpoint", action="store_true")
     ap.add_argument("--flash_attention", choices=["auto", "on", "off"], default="auto")
     args = ap.parse_args(argv)
+    from . import exact_fp32_convs
+    exact_fp32_convs()  # before any convolution (the fp32 / eval paths use MIOpen)
 
     info = init_from_env()
     cfg, env_d, model_d, extras = load_config(args.config)

@@ -14,6 +14,9 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 for p in (ROOT, PKG_DIR, os.path.join(ROOT, "oracle")):
     if p not in sys.path:
         sys.path.insert(0, p)
+# exact fp32 convolutions for the fp32 parity tests (ms_amd.exact_fp32_convs), set before MIOpen
+# runs anything; spawned test workers inherit it
+os.environ.setdefault("MIOPEN_DEBUG_CONV_WINOGRAD", "0")
 
 
 def pytest_configure(config):

@@ -23,7 +23,7 @@ def header_functions(headers=HEADERS, prefix="ms_"):
 def test_header_declares_expected_entry_points():
     fns = header_functions()
     for name in ("ms_create", "ms_destroy", "ms_reset", "ms_step", "ms_step_i32", "ms_labels",
-                 "ms_snapshot", "ms_tape_actions", "ms_gae", "ms_sample_masked", "ms_last_error",
+                 "ms_snapshot", "ms_tape_actions", "ms_gae", "ms_sample_masked", "ms_dropout_masks", "ms_last_error",
                  "ms_rng_state", "ms_abi_version"):
         assert name in fns
 

@@ -33,8 +33,16 @@ def _ref(x, w, b, g, be, H, W, res=None, dmask=None):
     return to_nhwc(z), to_nhwc(y), torch.stack([mean, rstd], -1)
 
 
+# Production sizes: one PPO minibatch per GPU at each BASELINE config --
+# C2/C4 16x16 (4096 envs x 64 steps / 8 = 32,768 samples; the stem too), C3 9x9 (8192 x 64 / 8 =
+# 65,536), C5 30x16 (1024 envs per GPU x 64 / 8 = 8,192). They take k_wgrad's sample-group split
+# and partial buffers, k_reduce's slicing and the grid sizes that the small cases never reach.
+PROD = [pytest.param(16, 16, 96, 32768, id="c2-16x16-32768"), pytest.param(16, 16, 16, 32768, id="c2-stem-32768"),
+        pytest.param(9, 9, 96, 65536, id="c3-9x9-65536"), pytest.param(30, 16, 96, 8192, id="c5-30x16-8192")]
+
+
 @pytest.mark.parametrize("H,W,cin,n", [(16, 16, 96, 300), (16, 16, 16, 37), (9, 9, 96, 70), (30, 16, 96, 20),
-                                       (16, 30, 96, 9), (5, 7, 16, 3)])
+                                       (16, 30, 96, 9), (5, 7, 16, 3)] + PROD)
 @pytest.mark.parametrize("with_res", [False, True])
 @pytest.mark.parametrize("dt", DT)
 def test_conv_gn_fwd_matches_torch(gpu, H, W, cin, n, with_res, dt):
@@ -73,7 +81,7 @@ def _gn(y, g, b):
 
 
 @pytest.mark.parametrize("H,W,cin,n", [(16, 16, 96, 300), (16, 16, 16, 37), (9, 9, 96, 70), (30, 16, 96, 20),
-                                       (5, 7, 16, 3), (8, 8, 96, 5), (16, 16, 96, 600)])
+                                       (5, 7, 16, 3), (8, 8, 96, 5), (16, 16, 96, 600)] + PROD)
 @pytest.mark.parametrize("with_res", [False, True])
 @pytest.mark.parametrize("dt", DT)
 def test_conv_gn_bwd_matches_torch(gpu, H, W, cin, n, with_res, dt):
@@ -150,7 +158,8 @@ def test_conv_gn_bwd_matches_torch(gpu, H, W, cin, n, with_res, dt):
         assert _rel(dx, nhwc(xq.grad) + (add.float() if add is not None else 0)) < 6e-2
 
 
-@pytest.mark.parametrize("n,P", [(300, 256), (7, 81), (3, 30)])
+@pytest.mark.parametrize("n,P", [(300, 256), (7, 81), (3, 30), pytest.param(32768, 256, id="c2-32768x256"),
+                                 pytest.param(65536, 81, id="c3-65536x81"), pytest.param(8192, 480, id="c5-8192x480")])
 @pytest.mark.parametrize("with_mine", [True, False])
 @pytest.mark.parametrize("dt", DT)
 def test_heads_match_torch(gpu, n, P, with_mine, dt):

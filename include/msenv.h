@@ -44,6 +44,8 @@ enum { MS_OUTCOME_NONE = 0, MS_OUTCOME_WIN = 1, MS_OUTCOME_LOSS = 2 };
 
 /* action-tape modes for ms_tape_actions (SURVEY.md §8d synthetic policy) */
 enum { MS_TAPE_UNIFORM = 0, MS_TAPE_SAFE_BIASED = 1 };
+/* Late-start generator modes (ms_set_late_start_mode). */
+enum { MS_LATE_SHARED = 0, MS_LATE_KEYED = 1 };
 
 /* Replaces EnvConfig (env.py:19-30). use_pair_constraints / solver_preset are
  * inert on the step path and therefore absent. Rewards are doubles: the
@@ -129,6 +131,18 @@ int ms_rng_state(ms_handle* h, uint64_t* out, void* stream);
  * requires its `done` output. */
 int ms_set_late_start(ms_handle* h, double prob, int32_t min_hidden, int32_t max_hidden,
                       int32_t max_attempts, int32_t max_extra_steps, uint64_t late_seed);
+
+/* Which generator the late starts draw from.
+ * MS_LATE_SHARED (default): the reference's ONE generator, consumed in env order
+ *   (env.py:397-403, 416-466). Each reset consumes a data-dependent number of
+ *   draws, so the resets of a step form one serial chain (one wave walks them).
+ *   Bit-exact with the reference on one handle; a shard draws its own stream.
+ * MS_LATE_KEYED: each reset draws from its own PCG64 stream keyed by (late_seed,
+ *   GLOBAL env index, the env's own generator state at the reset), so all of a
+ *   step's resets run at once (one wave per env) and a shard's resets are those of
+ *   the unsharded run. Same procedure and distribution as the reference; not the
+ *   reference's stream of draws (oracle: mso_set_late_start_mode). */
+int ms_set_late_start_mode(ms_handle* h, int32_t mode);
 
 /* The late-start generator's state as u64[6] (ms_rng_state layout); synchronous. */
 int ms_late_rng_state(ms_handle* h, uint64_t* out);

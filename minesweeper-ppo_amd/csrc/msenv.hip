@@ -1100,6 +1100,124 @@ struct LateCfg {
   int32_t min_hidden, max_hidden, max_attempts, max_extra_steps;
 };
 
+// The late-start generator of the keyed mode (MS_LATE_KEYED): a PCG64 state built from
+// (late seed, GLOBAL env index, the env's own PCG64 state at the reset) by splitmix64.
+// The env's own state advances every episode (each episode places its mines), so every
+// reset of every env has its own stream, independent of the world size and of the order
+// in which envs reset. oracle/ms_oracle.c (keyed_late_rng) restates it.
+__device__ __forceinline__ Pcg keyed_late_pcg(uint64_t seed, uint64_t gidx, uint64_t st_hi, uint64_t st_lo) {
+  Pcg L;
+  L.hi = splitmix64(seed ^ splitmix64(gidx ^ 0x6C8E9CF570932BD5ull));
+  L.lo = splitmix64(L.hi ^ st_lo);
+  L.ihi = splitmix64(L.lo ^ st_hi);
+  L.ilo = splitmix64(L.ihi ^ 0xA0761D6478BD642Full) | 1ull;
+  L.has32 = 0u;
+  L.uinteger = 0u;
+  return L;
+}
+
+// One env's _apply_late_start (env.py:421-466) with the late generator L (wave-uniform),
+// its clicks wave-parallel as in k_step; writes the env's state and its reset obs / mask.
+template <int H_, int W_>
+__device__ __forceinline__ void late_env(const KParams& p, Pcg& L, const LateCfg& lc, int64_t env,
+                                         const uint64_t (&J)[4], uint64_t* sR, uint64_t* sM, uint32_t* sTab,
+                                         const Geo<H_, W_>& g, int lane) {
+  const int H = g.H, W = g.W, A = g.A(), NW = g.NW();
+  const uint64_t rowmask = g.rowmask();
+  const int safe_total = A - p.K;
+  EnvMeta* mp = p.meta + env;
+  uint64_t* mwords = p.mine_words + env * NW;
+  uint64_t* rwords = p.rev_words + env * NW;
+  uint64_t mine = load_row(mwords, g, lane);
+  uint64_t rev = load_row(rwords, g, lane);
+  Pcg rng;
+  rng.hi = rfl64(mp->st_hi);
+  rng.lo = rfl64(mp->st_lo);
+  rng.ihi = rfl64(mp->inc_hi);
+  rng.ilo = rfl64(mp->inc_lo);
+  rng.has32 = rfl(mp->has32);
+  rng.uinteger = rfl(mp->uinteger);
+  int32_t step_count = (int32_t)rfl((uint32_t)mp->step_count);
+  bool fc = (rfl(mp->flags) & 1u) != 0;
+  // prob <= 0 short-circuits before the draw (env.py:421)
+  if (lc.prob > 0.0 && (double)(pcg_next64(L) >> 11) * 0x1.0p-53 < lc.prob) {
+    bool success = false;
+    for (int att = 0; att < lc.max_attempts && !success; ++att) {
+      if (fc) {  // env.reset() (env.py:87-101): the env's own RNG continues
+        mine = 0ull;
+        rev = 0ull;
+        fc = false;
+        step_count = 0;
+      }
+      const int first = (int)pcg_bounded(L, (uint32_t)(A - 1));
+      bool done, mc = false;
+      int oc;
+      uint32_t nw, tr;
+      board_click(rng, mine, rev, fc, first, p, J, sTab, sR, g, lane, done, oc, nw, tr, mc);
+      step_count += 1;
+      if (done) continue;
+      int target = lc.min_hidden + (int)pcg_bounded(L, (uint32_t)(lc.max_hidden - lc.min_hidden));
+      target = target < safe_total ? target : safe_total;
+      target = target > 1 ? target : 1;
+      int revealed = (int)tr;
+      for (int k = 0; k < lc.max_extra_steps; ++k) {
+        if (safe_total - revealed <= target) {
+          success = true;
+          break;
+        }
+        const uint64_t cand = ~mine & ~rev & (lane < H ? rowmask : 0ull);
+        const uint32_t pc = (uint32_t)__popcll(cand);
+        const uint32_t cnt = wave_sum(pc);
+        if (cnt == 0) break;
+        const uint32_t kk = pcg_bounded(L, cnt - 1u);  // rng.choice(flatnonzero(...)) (row-major)
+        const uint32_t before = wave_excl_scan(pc);
+        const bool mine_lane = kk >= before && kk < before + pc;
+        const uint64_t who = __ballot(mine_lane);
+        const int src = __ffsll((unsigned long long)who) - 1;
+        const int col = (int)readlane32((uint32_t)(mine_lane ? select_bit(cand, kk - before) : 0), src);
+        board_click(rng, mine, rev, fc, src * W + col, p, J, sTab, sR, g, lane, done, oc, nw, tr, mc);
+        step_count += 1;
+        revealed = (int)tr;
+        if (done) break;
+      }
+      if (!success && !done && safe_total - revealed <= target) success = true;
+    }
+    if (!success) {  // fallback: leave the board fresh (env.py:465-466)
+      mine = 0ull;
+      rev = 0ull;
+      fc = false;
+      step_count = 0;
+    }
+  }
+  if (lane == 0) {
+    mp->st_hi = rng.hi;
+    mp->st_lo = rng.lo;
+    mp->has32 = rng.has32;
+    mp->uinteger = rng.uinteger;
+    mp->step_count = step_count;
+    mp->flags = fc ? 1u : 0u;
+  }
+  store_rows(mwords, mine, sR, g, lane);
+  store_rows(rwords, rev, sR, g, lane);
+  __syncthreads();
+  if (p.obs || p.mask) {
+    stage_rows(sR, sM, rev, mine, g, lane);
+    emit_obs(p.obs ? p.obs + env * 10 * A : nullptr, p.mask ? p.mask + env * A : nullptr, sR, sM, fc, g, lane,
+             reinterpret_cast<uint8_t*>(sTab));
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void load_jump(const uint64_t* jump, int lane, uint64_t (&J)[4]) {
+  const ulonglong2* e = reinterpret_cast<const ulonglong2*>(jump + 4 * lane);
+  const ulonglong2 a0 = e[0], a1 = e[1];
+  J[0] = a0.x;
+  J[1] = a0.y;
+  J[2] = a1.x;
+  J[3] = a1.y;
+}
+
+// MS_LATE_SHARED (the reference): one wave walks the envs in order with the shared generator.
 template <int H_, int W_>
 __global__ __launch_bounds__(64) void k_late(KParams p, Pcg* lstate, LateCfg lc, const uint8_t* need) {
   __shared__ uint64_t sR[kWave];
@@ -1107,9 +1225,6 @@ __global__ __launch_bounds__(64) void k_late(KParams p, Pcg* lstate, LateCfg lc,
   __shared__ uint32_t sTab[(H_ && W_) ? H_ * W_ : kMaxH * kMaxW];
   const int lane = lane_id();
   const Geo<H_, W_> g(p.H, p.W);
-  const int H = g.H, W = g.W, A = g.A(), NW = g.NW();
-  const uint64_t rowmask = g.rowmask();
-  const int safe_total = A - p.K;
   Pcg L;
   L.hi = lstate->hi;
   L.lo = lstate->lo;
@@ -1118,97 +1233,10 @@ __global__ __launch_bounds__(64) void k_late(KParams p, Pcg* lstate, LateCfg lc,
   L.has32 = lstate->has32;
   L.uinteger = lstate->uinteger;
   uint64_t J[4];
-  {
-    const ulonglong2* e = reinterpret_cast<const ulonglong2*>(p.jump + 4 * lane);
-    const ulonglong2 a0 = e[0], a1 = e[1];
-    J[0] = a0.x;
-    J[1] = a0.y;
-    J[2] = a1.x;
-    J[3] = a1.y;
-  }
+  load_jump(p.jump, lane, J);
   for (int64_t env = 0; env < p.n; ++env) {
     if (need && !need[env]) continue;
-    EnvMeta* mp = p.meta + env;
-    uint64_t* mwords = p.mine_words + env * NW;
-    uint64_t* rwords = p.rev_words + env * NW;
-    uint64_t mine = load_row(mwords, g, lane);
-    uint64_t rev = load_row(rwords, g, lane);
-    Pcg rng;
-    rng.hi = rfl64(mp->st_hi);
-    rng.lo = rfl64(mp->st_lo);
-    rng.ihi = rfl64(mp->inc_hi);
-    rng.ilo = rfl64(mp->inc_lo);
-    rng.has32 = rfl(mp->has32);
-    rng.uinteger = rfl(mp->uinteger);
-    int32_t step_count = (int32_t)rfl((uint32_t)mp->step_count);
-    bool fc = (rfl(mp->flags) & 1u) != 0;
-    // prob <= 0 short-circuits before the draw (env.py:421)
-    if (lc.prob > 0.0 && (double)(pcg_next64(L) >> 11) * 0x1.0p-53 < lc.prob) {
-      bool success = false;
-      for (int att = 0; att < lc.max_attempts && !success; ++att) {
-        if (fc) {  // env.reset() (env.py:87-101): the env's own RNG continues
-          mine = 0ull;
-          rev = 0ull;
-          fc = false;
-          step_count = 0;
-        }
-        const int first = (int)pcg_bounded(L, (uint32_t)(A - 1));
-        bool done, mc = false;
-        int oc;
-        uint32_t nw, tr;
-        board_click(rng, mine, rev, fc, first, p, J, sTab, sR, g, lane, done, oc, nw, tr, mc);
-        step_count += 1;
-        if (done) continue;
-        int target = lc.min_hidden + (int)pcg_bounded(L, (uint32_t)(lc.max_hidden - lc.min_hidden));
-        target = target < safe_total ? target : safe_total;
-        target = target > 1 ? target : 1;
-        int revealed = (int)tr;
-        for (int k = 0; k < lc.max_extra_steps; ++k) {
-          if (safe_total - revealed <= target) {
-            success = true;
-            break;
-          }
-          const uint64_t cand = ~mine & ~rev & (lane < H ? rowmask : 0ull);
-          const uint32_t pc = (uint32_t)__popcll(cand);
-          const uint32_t cnt = wave_sum(pc);
-          if (cnt == 0) break;
-          const uint32_t kk = pcg_bounded(L, cnt - 1u);  // rng.choice(flatnonzero(...)) (row-major)
-          const uint32_t before = wave_excl_scan(pc);
-          const bool mine_lane = kk >= before && kk < before + pc;
-          const uint64_t who = __ballot(mine_lane);
-          const int src = __ffsll((unsigned long long)who) - 1;
-          const int col = (int)readlane32((uint32_t)(mine_lane ? select_bit(cand, kk - before) : 0), src);
-          board_click(rng, mine, rev, fc, src * W + col, p, J, sTab, sR, g, lane, done, oc, nw, tr, mc);
-          step_count += 1;
-          revealed = (int)tr;
-          if (done) break;
-        }
-        if (!success && !done && safe_total - revealed <= target) success = true;
-      }
-      if (!success) {  // fallback: leave the board fresh (env.py:465-466)
-        mine = 0ull;
-        rev = 0ull;
-        fc = false;
-        step_count = 0;
-      }
-    }
-    if (lane == 0) {
-      mp->st_hi = rng.hi;
-      mp->st_lo = rng.lo;
-      mp->has32 = rng.has32;
-      mp->uinteger = rng.uinteger;
-      mp->step_count = step_count;
-      mp->flags = fc ? 1u : 0u;
-    }
-    store_rows(mwords, mine, sR, g, lane);
-    store_rows(rwords, rev, sR, g, lane);
-    __syncthreads();
-    if (p.obs || p.mask) {
-      stage_rows(sR, sM, rev, mine, g, lane);
-      emit_obs(p.obs ? p.obs + env * 10 * A : nullptr, p.mask ? p.mask + env * A : nullptr, sR, sM, fc, g,
-               lane, reinterpret_cast<uint8_t*>(sTab));
-    }
-    __syncthreads();
+    late_env(p, L, lc, env, J, sR, sM, sTab, g, lane);
   }
   if (lane == 0) {
     lstate->hi = L.hi;
@@ -1216,6 +1244,25 @@ __global__ __launch_bounds__(64) void k_late(KParams p, Pcg* lstate, LateCfg lc,
     lstate->has32 = L.has32;
     lstate->uinteger = L.uinteger;
   }
+}
+
+// MS_LATE_KEYED: one wave per env, every resetting env at once, each with its own
+// keyed generator (keyed_late_pcg).
+template <int H_, int W_>
+__global__ __launch_bounds__(64) void k_late_keyed(KParams p, LateCfg lc, uint64_t seed, int64_t env_begin,
+                                                   const uint8_t* need) {
+  __shared__ uint64_t sR[kWave];
+  __shared__ uint64_t sM[kWave + 2];
+  __shared__ uint32_t sTab[(H_ && W_) ? H_ * W_ : kMaxH * kMaxW];
+  const int64_t env = blockIdx.x;
+  if (need && !need[env]) return;  // (uniform: one wave per workgroup)
+  const int lane = lane_id();
+  const Geo<H_, W_> g(p.H, p.W);
+  uint64_t J[4];
+  load_jump(p.jump, lane, J);
+  const EnvMeta* mp = p.meta + env;
+  Pcg L = keyed_late_pcg(seed, (uint64_t)(env_begin + env), rfl64(mp->st_hi), rfl64(mp->st_lo));
+  late_env(p, L, lc, env, J, sR, sM, sTab, g, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -1570,6 +1617,8 @@ struct ms_handle {
   hipEvent_t ev_start, ev_stop;  // ms_set_timing_events (measurement only): stamp k_step / k_run
   LateCfg late;
   Pcg* late_rng;   // device: the shared late-start generator
+  int late_mode;   // MS_LATE_SHARED (the reference's one generator) | MS_LATE_KEYED
+  uint64_t late_seed;
 };
 
 namespace {
@@ -1620,8 +1669,18 @@ void fill_params(const ms_handle* h, KParams& p) {
   p.dbg_flags = h->dbg_flags;
 }
 
+template <int H_, int W_>
+void launch_late_keyed_t(const KParams& p, const ms_handle* h, const uint8_t* need, hipStream_t s) {
+  hipLaunchKernelGGL((k_late_keyed<H_, W_>), dim3((unsigned)p.n), dim3(64), 0, s, p, h->late, h->late_seed,
+                     h->env_begin, need);
+}
+
 int launch_late(const ms_handle* h, const KParams& p, const uint8_t* need, hipStream_t s) {
-  if (h->H == 16 && h->W == 16) launch_late_t<16, 16>(p, h->late_rng, h->late, need, s);
+  if (h->late_mode == MS_LATE_KEYED) {
+    if (h->H == 16 && h->W == 16) launch_late_keyed_t<16, 16>(p, h, need, s);
+    else if (h->H == 9 && h->W == 9) launch_late_keyed_t<9, 9>(p, h, need, s);
+    else launch_late_keyed_t<0, 0>(p, h, need, s);
+  } else if (h->H == 16 && h->W == 16) launch_late_t<16, 16>(p, h->late_rng, h->late, need, s);
   else if (h->H == 9 && h->W == 9) launch_late_t<9, 9>(p, h->late_rng, h->late, need, s);
   else launch_late_t<0, 0>(p, h->late_rng, h->late, need, s);
   hipError_t e = hipGetLastError();
@@ -1840,6 +1899,14 @@ int ms_set_late_start(ms_handle* h, double prob, int32_t min_hidden, int32_t max
   if (e != hipSuccess) return hip_fail(e, "ms_set_late_start copy");
   h->late = c;
   h->late_on = 1;
+  h->late_seed = late_seed;
+  return MS_OK;
+}
+
+int ms_set_late_start_mode(ms_handle* h, int32_t mode) {
+  if (!h) return fail(MS_EINVAL, "ms_set_late_start_mode: null handle");
+  if (mode != MS_LATE_SHARED && mode != MS_LATE_KEYED) return fail(MS_EINVAL, "ms_set_late_start_mode: bad mode");
+  h->late_mode = mode;
   return MS_OK;
 }
 

@@ -21,6 +21,7 @@ ABI_VERSION = 2
 
 MS_OUTCOME_NONE, MS_OUTCOME_WIN, MS_OUTCOME_LOSS = 0, 1, 2
 MS_TAPE_UNIFORM, MS_TAPE_SAFE_BIASED = 0, 1
+MS_LATE_SHARED, MS_LATE_KEYED = 0, 1
 
 
 class MsEnvError(RuntimeError):
@@ -54,7 +55,8 @@ SIGNATURES = {
     "ms_gae": [_vp, _vp, _vp, _vp, _i32, _i64, _f32, _f32, _vp, _vp, _vp],
     "ms_sample_masked": [_vp, _vp, _i64, _i32, _i64, _u64, _u64, _vp, _vp, _vp],
     "ms_dropout_masks": [_vp, _i64, _i32, _i32, _u64, _u64, _f32, _vp, _vp],
-    "ms_set_late_start":[_vp, ctypes.c_double, _i32, _i32, _i32, _i32, _u64],
+    "ms_set_late_start": [_vp, ctypes.c_double, _i32, _i32, _i32, _i32, _u64],
+    "ms_set_late_start_mode": [_vp, _i32],
     "ms_late_rng_state": [_vp, _vp],
     # msenv_debug.h
     "ms_set_debug_flags": [_vp, ctypes.c_uint32],

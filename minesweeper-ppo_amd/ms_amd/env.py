@@ -161,6 +161,9 @@ class _EnvList:
         return (self[i] for i in range(len(self)))
 
 
+LATE_MODES = {"shared": 0, "keyed": 1}  # MS_LATE_SHARED / MS_LATE_KEYED
+
+
 class VecMinesweeper:
     """Batched Minesweeper with all board state in HBM (one HIP handle)."""
 
@@ -201,11 +204,20 @@ class VecMinesweeper:
                 late_start_seed = int(base.integers(0, 2**31 - 1))
             ls = self._late_start_cfg
             mn = int(ls.get("min_hidden", 5))
-            # a shard cannot replay the global env-order stream: it draws its own
-            lseed = int(late_start_seed) if world == 1 else (int(late_start_seed) * 1000003 + begin) % 2**63
+            # ls["rng"]: "shared" (default) = the reference's one generator, consumed in env order by
+            # one wave (bit-exact; a shard cannot replay the global stream and draws its own);
+            # "keyed" = one stream per reset keyed by global env (MS_LATE_KEYED, include/msenv.h):
+            # every reset of a step in parallel, and a shard's resets are the unsharded run's
+            mode = ls.get("rng", "shared")
+            if mode not in LATE_MODES:
+                raise ValueError(f"late_start_cfg rng must be one of {sorted(LATE_MODES)}, got {mode!r}")
+            keyed = LATE_MODES[mode] == L.MS_LATE_KEYED
+            lseed = int(late_start_seed) if (world == 1 or keyed) else \
+                (int(late_start_seed) * 1000003 + begin) % 2**63
             L.check(self._lib.ms_set_late_start(h, float(ls.get("prob", 0.0)), mn, int(ls.get("max_hidden", mn)),
                                                 int(ls.get("max_attempts", 3)),
                                                 int(ls.get("max_extra_steps", self.A)), lseed))
+            L.check(self._lib.ms_set_late_start_mode(h, LATE_MODES[mode]))
         self._version = 0
         self._snap = None
         self._snap_version = -1

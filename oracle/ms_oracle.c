@@ -256,6 +256,8 @@ struct mso_vec {
   int late_on;
   late_cfg_t late;
   pcg64_t late_rng;
+  int late_mode; /* 0 shared generator (the reference), 1 keyed per reset */
+  uint64_t late_seed;
 };
 typedef struct mso_vec mso_vec;
 
@@ -451,9 +453,33 @@ static void write_obs(const mso_vec* v, const env_t* e, float* obs, uint8_t* mas
     for (int i = 0; i < A; i++) mask[i] = (uint8_t)!e->revealed[i];
 }
 
+static inline uint64_t splitmix64(uint64_t x);
+
+/* MS_LATE_KEYED (include/msenv.h): the reset's own generator, keyed by (late seed, GLOBAL
+ * env index, the env's own PCG64 state at the reset) through splitmix64 (keyed_late_pcg in
+ * csrc/msenv.hip). A raw PCG64 state (no SeedSequence), has_uint32 = 0. */
+static pcg64_t keyed_late_rng(uint64_t seed, uint64_t gidx, const pcg64_t* env_rng) {
+  const uint64_t st_hi = (uint64_t)(env_rng->state >> 64), st_lo = (uint64_t)env_rng->state;
+  const uint64_t a = splitmix64(seed ^ splitmix64(gidx ^ 0x6C8E9CF570932BD5ULL));
+  const uint64_t b = splitmix64(a ^ st_lo);
+  const uint64_t c = splitmix64(b ^ st_hi);
+  const uint64_t d = splitmix64(c ^ 0xA0761D6478BD642FULL) | 1ULL;
+  pcg64_t r;
+  r.state = ((u128)a << 64) | b;
+  r.inc = ((u128)c << 64) | d;
+  r.has32 = 0;
+  r.uinteger = 0;
+  return r;
+}
+
 /* _apply_late_start (env.py:416-466) */
 static void apply_late_start(mso_vec* v, env_t* e, scratch_t* s) {
+  pcg64_t keyed;
   pcg64_t* rng = &v->late_rng;
+  if (v->late_mode == 1) {
+    keyed = keyed_late_rng(v->late_seed, (uint64_t)(v->env_begin + (e - v->envs)), &e->rng);
+    rng = &keyed;
+  }
   const late_cfg_t* L = &v->late;
   if (L->prob <= 0.0 || rng_random(rng) >= L->prob) return;
   int min_h = L->min_hidden < 1 ? 1 : L->min_hidden;
@@ -542,6 +568,16 @@ int mso_set_late_start(mso_vec* v, double prob, int32_t min_hidden, int32_t max_
   v->late.max_attempts = max_attempts;
   v->late.max_extra_steps = max_extra_steps;
   pcg_seed(&v->late_rng, late_seed);
+  v->late_seed = late_seed;
+  return MS_OK;
+}
+
+int mso_set_late_start_mode(mso_vec* v, int32_t mode) {
+  if (mode != 0 && mode != 1) {
+    snprintf(g_err, sizeof g_err, "mso_set_late_start_mode: bad mode");
+    return MS_EINVAL;
+  }
+  v->late_mode = mode;
   return MS_OK;
 }
 
@@ -619,7 +655,7 @@ static int step_impl(mso_vec* v, const int64_t* a64, const int32_t* a32, float* 
     snprintf(g_err, sizeof g_err, "mso_step: null argument");
     return MS_EINVAL;
   }
-  if (nthreads < 1 || v->late_on) nthreads = 1;
+  if (nthreads < 1 || (v->late_on && v->late_mode == 0)) nthreads = 1; /* the shared generator is a serial chain */
   if (nthreads > v->n) nthreads = (int)v->n;
   step_job_t jobs[256];
   pthread_t th[256];
@@ -775,7 +811,7 @@ int mso_run_baseline(mso_vec* v, uint64_t t0, int64_t steps, int32_t mode, int32
     snprintf(g_err, sizeof g_err, "mso_run_baseline: bad argument");
     return MS_EINVAL;
   }
-  if (nthreads < 1 || v->late_on) nthreads = 1;
+  if (nthreads < 1 || (v->late_on && v->late_mode == 0)) nthreads = 1; /* the shared generator is a serial chain */
   if (nthreads > v->n) nthreads = (int)v->n;
   if (nthreads > 1024) nthreads = 1024;
   run_job_t* jobs = (run_job_t*)calloc((size_t)nthreads, sizeof(run_job_t));

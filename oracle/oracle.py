@@ -45,6 +45,7 @@ def lib():
         L.mso_destroy.argtypes = [vp]
         L.mso_destroy.restype = None
         L.mso_set_late_start.argtypes = [vp, ctypes.c_double, i32, i32, i32, i32, u64]
+        L.mso_set_late_start_mode.argtypes = [vp, i32]
         L.mso_reset.argtypes = [vp, vp, vp]
         L.mso_step.argtypes = [vp] + [vp] * 9 + [i32]
         L.mso_step_i32.argtypes = [vp] + [vp] * 9 + [i32]
@@ -77,6 +78,10 @@ def _check(rc):
         raise RuntimeError(lib().mso_last_error().decode())
 
 
+# late_start_cfg["rng"]: "shared" = the reference's one generator; "keyed" = MS_LATE_KEYED
+LATE_MODES = {"shared": 0, "keyed": 1}
+
+
 class OracleVec:
     """Same state machine as VecMinesweeper, host arrays, one C call per method."""
 
@@ -98,6 +103,7 @@ class OracleVec:
                                      int(ls.get("max_attempts", 3)),
                                      int(ls.get("max_extra_steps", H * W)),
                                      int(late_seed if late_seed is not None else seed + 1))
+            _check(lib().mso_set_late_start_mode(h, LATE_MODES[ls.get("rng", "shared")]))
 
     def __del__(self):
         if getattr(self, "_h", None) is not None and _lib is not None:

@@ -96,6 +96,34 @@ def test_late_start_matches_oracle(gpu, H, W, K, N):
     _diff_run(H, W, K, N, T=60, mode=1, seed=5, check_every=3, labels=False, late=late)
 
 
+@pytest.mark.parametrize("H,W,K,N", [(16, 16, 40, 256), (9, 9, 10, 300), (30, 16, 99, 64), (7, 11, 20, 64)])
+def test_late_start_keyed_matches_oracle(gpu, H, W, K, N):
+    """MS_LATE_KEYED (one stream per reset, one wave per env, all resets of a step at once)
+    vs the oracle's restatement of the same rule (keyed_late_rng): bit-exact."""
+    late = dict(prob=0.6, min_hidden=3, max_hidden=2 * K, max_attempts=2, rng="keyed")
+    _diff_run(H, W, K, N, T=60, mode=1, seed=5, check_every=3, labels=False, late=late)
+
+
+def test_late_start_keyed_sharded_equals_unsharded(gpu):
+    """Keyed late starts depend on the GLOBAL env index only: two shards of a 512-env list
+    step exactly as the unsharded handle (the shared mode cannot: its stream is env-ordered)."""
+    from ms_amd import EnvConfig, VecMinesweeper
+    late = dict(prob=0.7, min_hidden=3, max_hidden=60, rng="keyed")
+    cfg = EnvConfig(H=16, W=16, mine_count=40)
+    full = VecMinesweeper(512, cfg, seed=4, late_start_cfg=late, late_start_seed=9)
+    parts = [VecMinesweeper(512, cfg, seed=4, late_start_cfg=late, late_start_seed=9, shard=(r, 2)) for r in range(2)]
+    obs = [full.reset()["obs"]] + [p.reset()["obs"] for p in parts]
+    assert torch.equal(obs[0], torch.cat(obs[1:]))
+    for t in range(40):
+        a = full.tape_actions(t, 1)
+        b_full, r_full, d_full, _ = full.step(a)
+        outs = [p.step(p.tape_actions(t, 1)) for p in parts]
+        assert torch.equal(b_full["obs"], torch.cat([o[0]["obs"] for o in outs])), t
+        assert torch.equal(r_full, torch.cat([o[1] for o in outs])), t
+        assert torch.equal(d_full, torch.cat([o[2] for o in outs])), t
+    assert np.array_equal(full.rng_state(), np.concatenate([p.rng_state() for p in parts]))
+
+
 @pytest.mark.parametrize("H,W,K", [(16, 16, 40), (9, 9, 10), (30, 16, 99), (16, 30, 99), (8, 8, 10)])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_diff_vs_oracle_benchmark_shapes(gpu, H, W, K, mode):

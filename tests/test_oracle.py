@@ -169,3 +169,44 @@ def test_cpu_baseline_runner_equals_step_loop():
     sa, sb = a.snapshot(), b.snapshot()
     for k in sa:
         assert np.array_equal(sa[k], sb[k]), k
+
+
+def _late_run(late, n=64, begin=0, count=None, T=40, nthreads=1):
+    v = O.OracleVec(16, 16, 40, n, seed=3, env_begin=begin, env_count=count, late_start=late, late_seed=7)
+    out = [v.reset()[0]]
+    for t in range(T):
+        a = v.tape(t, 1)
+        out.append(v.step(a, nthreads=nthreads)["obs"])
+    return np.stack(out), v.rng_state()
+
+
+def test_keyed_late_start_sharded_and_threaded_equal_unsharded():
+    """MS_LATE_KEYED restated in the oracle: a reset's stream depends on (seed, GLOBAL env, the
+    env's own generator state) only, so shards and threads reproduce the unsharded serial run."""
+    late = dict(prob=0.7, min_hidden=3, max_hidden=60, rng="keyed")
+    full, st = _late_run(late)
+    parts = [_late_run(late, begin=b, count=32) for b in (0, 32)]
+    assert np.array_equal(full, np.concatenate([p[0] for p in parts], axis=1))
+    assert np.array_equal(st, np.concatenate([p[1] for p in parts]))
+    thr, st_thr = _late_run(late, nthreads=4)
+    assert np.array_equal(full, thr) and np.array_equal(st, st_thr)
+    shared, _ = _late_run(dict(late, rng="shared"))
+    assert not np.array_equal(full, shared)  # a different stream of draws
+
+
+def test_keyed_late_start_same_distribution_as_shared():
+    """Same procedure (env.py:416-466), different draws: over 2,000 resets the fraction of
+    late-started boards and the mean number of revealed cells agree with the shared generator."""
+    stats = {}
+    for mode in ("shared", "keyed"):
+        v = O.OracleVec(16, 16, 40, 2000, seed=1, late_start=dict(prob=0.5, min_hidden=5, max_hidden=80, rng=mode),
+                        late_seed=11)
+        v.reset()
+        snap = v.snapshot()
+        started = snap["first_click"].astype(bool)
+        rev = snap["revealed"].reshape(2000, -1).sum(1)
+        stats[mode] = (started.mean(), rev[started].mean(), (256 - 40 - rev[started]).max())
+    (f_s, r_s, h_s), (f_k, r_k, h_k) = stats["shared"], stats["keyed"]
+    assert abs(f_s - 0.5) < 0.05 and abs(f_k - 0.5) < 0.05, (f_s, f_k)
+    assert abs(r_s - r_k) < 0.05 * r_s, (r_s, r_k)
+    assert h_s <= 80 and h_k <= 80  # every late-started board ends within max_hidden safe cells

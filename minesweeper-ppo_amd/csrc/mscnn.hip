@@ -402,9 +402,12 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
 // ~176 KB of HBM traffic, so compute and memory are balanced near both floors.
 // MODE: 0 no residual / dropout, 1 residual (second conv of a block), 2 dropout (first).
 // ------------------------------------------------------------------------------------
+#ifndef MC_WR_EXP
+#define MC_WR_EXP 0
+#endif
 constexpr int WR_P = 256, WR_CINP = 104, WR_XB = (WR_P + 1) * WR_CINP;  // x buffer (elements)
 constexpr int WR_NSLOT = WR_P * 13 / 64;  // 52 LDS-DMA wave-instructions per input tile
-constexpr size_t WR_LDS = (size_t)(2 * WR_XB + WR_P * COUT) * 2 + (2 * COUT + 2 * NGRP) * 4;
+constexpr size_t WR_LDS = (size_t)(2 * WR_XB + WR_P * COUT) * 2 + (4 * COUT + 2 * NGRP) * 4;
 
 template <typename E>
 __device__ __forceinline__ void wr_compute(const FwdParams<E>& p, const E* sX, E* sY, float* sSt, int w, int lane,
@@ -420,7 +423,6 @@ __device__ __forceinline__ void wr_compute(const FwdParams<E>& p, const E* sX, E
       Bw[tap][ks] = __builtin_bit_cast(
           E8, *reinterpret_cast<const u32x4*>(&p.wt[((size_t)tap * COUT + co) * COUT + ks * 16 + 8 * hh]));
   const float bias = p.bias[co];
-  const int rl = l32 >> 4, cl = l32 & 15;
   const float inv_cnt = 1.0f / (16.0f * (float)WR_P);
   lds_barrier();  // BAR_0: the first input tiles are staged
   for (int k = 0; k < cnt; ++k) {
@@ -430,19 +432,25 @@ __device__ __forceinline__ void wr_compute(const FwdParams<E>& p, const E* sX, E
     for (int t = 0; t < 8; ++t)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+#if MC_WR_EXP == 2  // timing experiment: no convolution (the memory wave alone)
+    if (k < 0)
+#endif
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int dr = tap / 3 - 1, dc = tap % 3 - 1;
-      const bool cv = (unsigned)(cl + dc) < 16u;
       // opaque per-tap base: the same LDS address recurs at another (tap, tile) pair
       // (row 2t + 1 = row 2(t+1) - 1); left visible, the compiler keeps such reads live across
       // taps and spills them
+      // (the per-tile offsets are recomputed per tap from an opaque lane copy: hoisted out of
+      // the sample loop, the 72 of them would take the registers the weights need)
       const E* Xt = X + opaque0();
+      const int lo = l32 + opaque0(), rlt = lo >> 4, clt = lo & 15;
+      const bool cv = (unsigned)(clt + dc) < 16u;
       int off[8];
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
-        const int r = 2 * t + rl + dr;
-        off[t] = (cv && (unsigned)r < 16u ? r * 16 + cl + dc : WR_P) * WR_CINP;
+        const int r = 2 * t + rlt + dr;
+        off[t] = (cv && (unsigned)r < 16u ? r * 16 + clt + dc : WR_P) * WR_CINP;
       }
       // 48 steps s = (ks, t), A operands through a ring of 4: step s+3's LDS read is issued
       // before step s's MFMA, the order pinned (left alone, the scheduler reuses one register
@@ -527,7 +535,7 @@ __device__ __forceinline__ void wr_stage(const FwdParams<E>& p, E* sX, int k, in
 // Epilogue of local sample k from the staged y and statistics (the memory wave).
 template <typename E, int MODE>
 __device__ __forceinline__ void wr_epilogue(const FwdParams<E>& p, const E* sY, const float* sGB, const float* sSt,
-                                            int k, int lane, bool staged) {
+                                            float* sCo, int k, int lane, bool staged) {
   typedef typename EV<E>::v8 E8;
   const int n = (int)blockIdx.x + k * (int)gridDim.x;
   constexpr int NCH = WR_P * 12 / 64;  // 48 16-B chunks per lane
@@ -537,35 +545,29 @@ __device__ __forceinline__ void wr_epilogue(const FwdParams<E>& p, const E* sY, 
 #pragma unroll
     for (int j = 0; j < NCH; ++j) rq[j] = rs[lane + 64 * j];
   }
-  float dm[3][8];
-  if (MODE == 2) {
-#pragma unroll
-    for (int j3 = 0; j3 < 3; ++j3) {
-      const int cg = (lane + 4 * j3) % 12;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dm[j3][j] = p.dmask[(size_t)n * COUT + cg * 8 + j];
-    }
-  }
   // every load of this sample (and the LDS-DMA of the tile two samples ahead) completes before
   // the first store is issued: a wait behind those stores would drain them
-  (void)staged;
+  float dmv[2] = {1.f, 1.f};
+  if (MODE == 2) {
+    dmv[0] = p.dmask[(size_t)n * COUT + lane];
+    if (lane < COUT - 64) dmv[1] = p.dmask[(size_t)n * COUT + 64 + lane];
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  // scale / shift of this lane's three channel groups (chunk c = lane + 64 j: group (lane + 4 j) % 12)
-  float ca[3][8], cb[3][8];
+  // scale / shift per channel (channels lane and lane + 64) into LDS; a chunk reads its 8
+  // (the registers go to the residual chunks)
 #pragma unroll
-  for (int j3 = 0; j3 < 3; ++j3) {
-    const int cg = (lane + 4 * j3) % 12, g = cg >> 1;
-    const float mu = sSt[2 * g], rs = sSt[2 * g + 1];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = cg * 8 + j;
+  for (int h = 0; h < 2; ++h) {
+    const int c = lane + 64 * h;
+    if (c < COUT) {
+      const int g = c >> 4;
+      const float mu = sSt[2 * g], rs = sSt[2 * g + 1];
       float a = sGB[c] * rs, b = sGB[COUT + c] - mu * a;
       if (MODE == 2) {  // relu(z) * d = relu(z * d) for d >= 0
-        a *= dm[j3][j];
-        b *= dm[j3][j];
+        a *= dmv[h];
+        b *= dmv[h];
       }
-      ca[j3][j] = a;
-      cb[j3][j] = b;
+      sCo[c] = a;
+      sCo[COUT + c] = b;
     }
   }
   if (p.stats && lane < NGRP) {
@@ -578,12 +580,24 @@ __device__ __forceinline__ void wr_epilogue(const FwdParams<E>& p, const E* sY, 
     const int c = lane + 64 * j;
     const u32x4 yv = *reinterpret_cast<const u32x4*>(&sY[c * 8]);
     if (p.ysave) *reinterpret_cast<u32x4*>(&p.ysave[base + (size_t)c * 8]) = yv;
+#if MC_WR_EXP == 1  // timing experiment: no epilogue arithmetic (out = y)
+    *reinterpret_cast<u32x4*>(&p.out[base + (size_t)c * 8]) = yv;
+    if (p.rmask) p.rmask[(size_t)n * WR_P * 12 + c] = 0xffu;
+    continue;
+#endif
     const E8 y8 = __builtin_bit_cast(E8, yv);
+    const int cg = (lane + 4 * (j % 3)) % 12;
+    const float4 a0 = *reinterpret_cast<const float4*>(&sCo[cg * 8]);
+    const float4 a1 = *reinterpret_cast<const float4*>(&sCo[cg * 8 + 4]);
+    const float4 b0 = *reinterpret_cast<const float4*>(&sCo[COUT + cg * 8]);
+    const float4 b1 = *reinterpret_cast<const float4*>(&sCo[COUT + cg * 8 + 4]);
+    const float ca[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const float cb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
     E8 o8;
     uint32_t mb = 0u;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float z = (float)y8[e] * ca[j % 3][e] + cb[j % 3][e];
+      float z = (float)y8[e] * ca[e] + cb[e];
       if (MODE == 1) z += (float)__builtin_bit_cast(E8, rq[j])[e];
       o8[e] = (E)fmaxf(z, 0.f);
       mb |= ((float)o8[e] > 0.f ? 1u : 0u) << e;
@@ -595,7 +609,7 @@ __device__ __forceinline__ void wr_epilogue(const FwdParams<E>& p, const E* sY, 
 
 template <typename E, int MODE>
 __device__ __forceinline__ void wr_memory(const FwdParams<E>& p, E* sX, const E* sY, const float* sGB,
-                                          const float* sSt, int lane, int cnt) {
+                                          const float* sSt, float* sCo, int lane, int cnt) {
   wr_stage(p, sX, 0, lane);
   if (cnt > 1) wr_stage(p, sX, 1, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -603,12 +617,12 @@ __device__ __forceinline__ void wr_memory(const FwdParams<E>& p, E* sX, const E*
   for (int k = 0; k < cnt; ++k) {
     if (k >= 1) {  // between BAR_2(k-1) and BAR_1(k): tile k+1 into the buffer conv k-1 freed
       if (k + 1 < cnt) wr_stage(p, sX, k + 1, lane);
-      wr_epilogue<E, MODE>(p, sY, sGB, sSt, k - 1, lane, k + 1 < cnt);
+      wr_epilogue<E, MODE>(p, sY, sGB, sSt, sCo, k - 1, lane, k + 1 < cnt);
     }
     lds_barrier();  // BAR_1(k)
     lds_barrier();  // BAR_2(k)
   }
-  wr_epilogue<E, MODE>(p, sY, sGB, sSt, cnt - 1, lane, false);
+  wr_epilogue<E, MODE>(p, sY, sGB, sSt, sCo, cnt - 1, lane, false);
 }
 
 template <typename E, int MODE>
@@ -618,6 +632,7 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd_wr(FwdParams<E> p) {
   E* sY = sX + 2 * WR_XB;                                          // [256][96]
   float* sGB = reinterpret_cast<float*>(sY + WR_P * COUT);         // gamma | beta
   float* sSt = sGB + 2 * COUT;                                     // [6][2] mean, rstd
+  float* sCo = sSt + 2 * NGRP;                                     // [2][96] scale, shift (memory wave)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int cnt = ((int)p.N - 1 - (int)blockIdx.x) / (int)gridDim.x + 1;  // grid <= N: cnt >= 1
@@ -628,7 +643,7 @@ __global__ __launch_bounds__(256, 1) void k_conv_gn_fwd_wr(FwdParams<E> p) {
     sGB[COUT + i] = p.beta[i];
   }
   if (wave < 3) wr_compute<E>(p, sX, sY, sSt, wave, lane, cnt);
-  else wr_memory<E, MODE>(p, sX, sY, sGB, sSt, lane, cnt);
+  else wr_memory<E, MODE>(p, sX, sY, sGB, sSt, sCo, lane, cnt);
 }
 
 template <typename E, int MODE>

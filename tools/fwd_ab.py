@@ -16,6 +16,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=32768)
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--dtypes", default="fp16,bf16")
+ap.add_argument("--modes", default="res,dropout,plain")
 args = ap.parse_args()
 dev = torch.device("cuda")
 n, H, W, P = args.n, 16, 16, 256
@@ -35,14 +37,15 @@ def timed(fn, iters):
     return e0.elapsed_time(e1) / iters
 
 
-for dt in (torch.float16, torch.bfloat16):
+for dt in [{"fp16": torch.float16, "bf16": torch.bfloat16}[d] for d in args.dtypes.split(",")]:
     x = (torch.randn(n, P, 96, device=dev) * 0.5).to(dt)
     w = torch.randn(96, 96, 3, 3, device=dev) * 0.03
     b, g, be = torch.randn(96, device=dev) * 0.1, 1 + 0.1 * torch.randn(96, device=dev), 0.1 * torch.randn(96, device=dev)
     wt = prep_weight(w, 96, dt)
     res = torch.randn(n, P, 96, device=dev).to(dt)
     dm = (torch.rand(n, 96, device=dev) > 0.05).float() / 0.95
-    for mode, kw in (("res", dict(res=res)), ("dropout", dict(dmask=dm)), ("plain", {})):
+    for mode, kw in [(m, {"res": dict(res=res), "dropout": dict(dmask=dm), "plain": {}}[m])
+                     for m in args.modes.split(",")]:
         outs, times = {}, {"auto": [], "per_sample": []}
         for rep in range(args.reps):
             for impl in ("per_sample", "auto"):

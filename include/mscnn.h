@@ -40,15 +40,6 @@ int mc_conv_gn_fwd(const uint16_t* x, const uint16_t* w, const float* bias, cons
                    uint16_t* ysave, float* stats, uint8_t* relu_mask, int32_t n, int32_t h, int32_t w_,
                    int32_t cin, float eps, int32_t dtype, void* stream);
 
-/* Measurement / A-B only (process-wide, not thread-safe): which forward kernel
- * mc_conv_gn_fwd runs. MC_FWD_AUTO (default): the weight-resident wave-specialised
- * kernel for 16x16 boards with 96 input channels (unless res and dmask are both
- * given), the per-sample kernel otherwise. MC_FWD_PER_SAMPLE: always the per-sample
- * kernel. Both compute the same layer (tests/test_fused_gpu.py checks each). */
-#define MC_FWD_AUTO 0
-#define MC_FWD_PER_SAMPLE 1
-int mc_set_fwd_impl(int32_t impl);
-
 /* Backward of one fused layer (the forward above with the same n, h, w, cin).
  * Inputs: dout = dL/d(out); out (or its relu_mask; the other may be NULL), ysave, stats
  * from the forward; x = the forward's

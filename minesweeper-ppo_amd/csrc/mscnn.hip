@@ -379,291 +379,6 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
 #endif
 }
 
-// ------------------------------------------------------------------------------------
-// k_conv_gn_fwd_wr: 16x16 boards, 96 -> 96 channels (every residual-block conv of the
-// shipped model), weights RESIDENT IN REGISTERS and the waves specialised.
-//
-// The per-sample kernel above re-stages all 9 weight taps (166 KB) through LDS for every
-// sample, behind 18 workgroup barriers, and its epilogue stores share the vmcnt queue with
-// the next sample's loads. Here one workgroup per CU holds, for the whole launch:
-//   waves 0-2 (compute): output channels 32w..32w+31 of every pixel. Their B operands
-//     (W[tap][co][ci] for their 32 channels, all 9 taps x 96 ci: 54 x 16 B per lane) are
-//     loaded once into VGPRs; per sample they run 9 x 6 x 8 = 432 v_mfma_f32_32x32x16 on
-//     the LDS input tile (A = 32 pixels x 16 ci, out-of-board taps read a zero row), then
-//     the GroupNorm statistics of their two whole groups in-wave (no exchange), and stage
-//     y (16-bit) in LDS. They issue no global memory operation after the weight load.
-//   wave 3 (memory): stages input tiles two samples ahead into a double-buffered LDS image
-//     with global_load_lds (LDS-DMA, no registers), and runs the epilogue of the previous
-//     sample from the staged y: scale / shift, residual or dropout, ReLU, and the stores
-//     of y, out and the ReLU bitmask. Its stores never sit in front of a compute wave's
-//     wait.
-// Two raw LDS barriers per sample hand the y staging buffer over (no vmcnt drain).
-// MFMA peak is 3 of 4 SIMDs; per sample and CU that is 13.8k cycles of MFMA against
-// ~176 KB of HBM traffic, so compute and memory are balanced near both floors.
-// MODE: 0 no residual / dropout, 1 residual (second conv of a block), 2 dropout (first).
-// ------------------------------------------------------------------------------------
-#ifndef MC_WR_EXP
-#define MC_WR_EXP 0
-#endif
-constexpr int WR_P = 256, WR_CINP = 104, WR_XB = (WR_P + 1) * WR_CINP;  // x buffer (elements)
-constexpr int WR_NSLOT = WR_P * 13 / 64;  // 52 LDS-DMA wave-instructions per input tile
-constexpr size_t WR_LDS = (size_t)(2 * WR_XB + WR_P * COUT) * 2 + (4 * COUT + 2 * NGRP) * 4;
-
-template <typename E>
-__device__ __forceinline__ void wr_compute(const FwdParams<E>& p, const E* sX, E* sY, float* sSt, int w, int lane,
-                                           int cnt) {
-  typedef typename EV<E>::v8 E8;
-  const int l32 = lane & 31, hh = lane >> 5;
-  const int co = 32 * w + l32;
-  E8 Bw[9][6];
-#pragma unroll
-  for (int tap = 0; tap < 9; ++tap)
-#pragma unroll
-    for (int ks = 0; ks < 6; ++ks)
-      Bw[tap][ks] = __builtin_bit_cast(
-          E8, *reinterpret_cast<const u32x4*>(&p.wt[((size_t)tap * COUT + co) * COUT + ks * 16 + 8 * hh]));
-  const float bias = p.bias[co];
-  const float inv_cnt = 1.0f / (16.0f * (float)WR_P);
-  lds_barrier();  // BAR_0: the first input tiles are staged
-  for (int k = 0; k < cnt; ++k) {
-    const E* X = sX + (k & 1) * WR_XB + 8 * hh;
-    f32x16 acc[8];
-#pragma unroll
-    for (int t = 0; t < 8; ++t)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
-#if MC_WR_EXP == 2  // timing experiment: no convolution (the memory wave alone)
-    if (k < 0)
-#endif
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int dr = tap / 3 - 1, dc = tap % 3 - 1;
-      // opaque per-tap base: the same LDS address recurs at another (tap, tile) pair
-      // (row 2t + 1 = row 2(t+1) - 1); left visible, the compiler keeps such reads live across
-      // taps and spills them
-      // (the per-tile offsets are recomputed per tap from an opaque lane copy: hoisted out of
-      // the sample loop, the 72 of them would take the registers the weights need)
-      const E* Xt = X + opaque0();
-      const int lo = l32 + opaque0(), rlt = lo >> 4, clt = lo & 15;
-      const bool cv = (unsigned)(clt + dc) < 16u;
-      int off[8];
-#pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const int r = 2 * t + rlt + dr;
-        off[t] = (cv && (unsigned)r < 16u ? r * 16 + clt + dc : WR_P) * WR_CINP;
-      }
-      // 48 steps s = (ks, t), A operands through a ring of 4: step s+3's LDS read is issued
-      // before step s's MFMA, the order pinned (left alone, the scheduler reuses one register
-      // set and waits out every read before its MFMA)
-      E8 a[4];
-#pragma unroll
-      for (int s0 = 0; s0 < 3; ++s0) a[s0] = *reinterpret_cast<const E8*>(Xt + off[s0 & 7] + (s0 >> 3) * 16);
-      __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
-#pragma unroll
-      for (int st = 0; st < 48; ++st) {
-        if (st + 3 < 48) {
-          const int s3 = st + 3;
-          a[s3 & 3] = *reinterpret_cast<const E8*>(Xt + off[s3 & 7] + (s3 >> 3) * 16);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
-        acc[st & 7] = mfma32(a[st & 3], Bw[tap][st >> 3], acc[st & 7]);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      }
-    }
-    // GroupNorm statistics, two-pass, of this lane's group (channels 32w + 16 * (l32 >> 4) ..):
-    // in-lane sums (8 chains), DPP row sums, the two lane halves (hh) by readlane
-    float gm[2], gr[2];
-#pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-      const float mu = pass ? (l32 < 16 ? gm[0] : gm[1]) : 0.f;
-      float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int t = 0; t < 8; ++t)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float d = acc[t][i] + bias - mu;
-          s[i & 7] += pass ? d * d : d;
-        }
-      const float part = row_sum16(((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7])));
-      const float lo = readlane_f(part, 15) + readlane_f(part, 47);
-      const float hi = readlane_f(part, 31) + readlane_f(part, 63);
-      if (pass == 0) {
-        gm[0] = lo * inv_cnt;
-        gm[1] = hi * inv_cnt;
-      } else {
-        gr[0] = rsqrtf(lo * inv_cnt + p.eps);
-        gr[1] = rsqrtf(hi * inv_cnt + p.eps);
-      }
-    }
-    lds_barrier();  // BAR_1(k): the memory wave is done with y / stats of sample k-1
-#pragma unroll
-    for (int t = 0; t < 8; ++t)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int px = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * hh;
-        sY[px * COUT + co] = (E)(acc[t][i] + bias);
-      }
-    if (lane == 0) {
-      sSt[4 * w + 0] = gm[0];
-      sSt[4 * w + 1] = gr[0];
-      sSt[4 * w + 2] = gm[1];
-      sSt[4 * w + 3] = gr[1];
-    }
-    lds_barrier();  // BAR_2(k): y_k staged; input buffer k & 1 is free
-  }
-}
-
-// one 16-B LDS-DMA per lane: global src (per lane) -> LDS dst + 16 * lane (dst wave-uniform)
-__device__ __forceinline__ void glds16(const void* src, void* dst) { __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0); }
-
-// LDS-DMA of local sample k's input tile [256][96] into the padded image [257][104]: slot u
-// (16 B) of the image holds pixel u / 13, chunk u % 13; chunk 12 is padding (loads a dummy
-// chunk of the same pixel, never read).
-template <typename E>
-__device__ __forceinline__ void wr_stage(const FwdParams<E>& p, E* sX, int k, int lane) {
-  const int n = (int)blockIdx.x + k * (int)gridDim.x;
-  const E* xs = p.x + (size_t)n * WR_P * COUT;
-  E* dst = sX + (k & 1) * WR_XB;
-#pragma unroll 4
-  for (int j = 0; j < WR_NSLOT; ++j) {
-    const int u = j * 64 + lane, r = u / 13, c = u - r * 13;
-    const E* src = xs + r * COUT + (c < 12 ? c * 8 : 0);
-    glds16(src, dst + j * 512);
-  }
-}
-
-// Epilogue of local sample k from the staged y and statistics (the memory wave).
-template <typename E, int MODE>
-__device__ __forceinline__ void wr_epilogue(const FwdParams<E>& p, const E* sY, const float* sGB, const float* sSt,
-                                            float* sCo, int k, int lane, bool staged) {
-  typedef typename EV<E>::v8 E8;
-  const int n = (int)blockIdx.x + k * (int)gridDim.x;
-  constexpr int NCH = WR_P * 12 / 64;  // 48 16-B chunks per lane
-  u32x4 rq[MODE == 1 ? NCH : 1];
-  if (MODE == 1) {
-    const u32x4* rs = reinterpret_cast<const u32x4*>(p.res + (size_t)n * WR_P * COUT);
-#pragma unroll
-    for (int j = 0; j < NCH; ++j) rq[j] = rs[lane + 64 * j];
-  }
-  // every load of this sample (and the LDS-DMA of the tile two samples ahead) completes before
-  // the first store is issued: a wait behind those stores would drain them
-  float dmv[2] = {1.f, 1.f};
-  if (MODE == 2) {
-    dmv[0] = p.dmask[(size_t)n * COUT + lane];
-    if (lane < COUT - 64) dmv[1] = p.dmask[(size_t)n * COUT + 64 + lane];
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  // scale / shift per channel (channels lane and lane + 64) into LDS; a chunk reads its 8
-  // (the registers go to the residual chunks)
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int c = lane + 64 * h;
-    if (c < COUT) {
-      const int g = c >> 4;
-      const float mu = sSt[2 * g], rs = sSt[2 * g + 1];
-      float a = sGB[c] * rs, b = sGB[COUT + c] - mu * a;
-      if (MODE == 2) {  // relu(z) * d = relu(z * d) for d >= 0
-        a *= dmv[h];
-        b *= dmv[h];
-      }
-      sCo[c] = a;
-      sCo[COUT + c] = b;
-    }
-  }
-  if (p.stats && lane < NGRP) {
-    p.stats[((size_t)n * NGRP + lane) * 2 + 0] = sSt[2 * lane];
-    p.stats[((size_t)n * NGRP + lane) * 2 + 1] = sSt[2 * lane + 1];
-  }
-  const size_t base = (size_t)n * WR_P * COUT;
-#pragma unroll
-  for (int j = 0; j < NCH; ++j) {
-    const int c = lane + 64 * j;
-    const u32x4 yv = *reinterpret_cast<const u32x4*>(&sY[c * 8]);
-    if (p.ysave) *reinterpret_cast<u32x4*>(&p.ysave[base + (size_t)c * 8]) = yv;
-#if MC_WR_EXP == 1  // timing experiment: no epilogue arithmetic (out = y)
-    *reinterpret_cast<u32x4*>(&p.out[base + (size_t)c * 8]) = yv;
-    if (p.rmask) p.rmask[(size_t)n * WR_P * 12 + c] = 0xffu;
-    continue;
-#endif
-    const E8 y8 = __builtin_bit_cast(E8, yv);
-    const int cg = (lane + 4 * (j % 3)) % 12;
-    const float4 a0 = *reinterpret_cast<const float4*>(&sCo[cg * 8]);
-    const float4 a1 = *reinterpret_cast<const float4*>(&sCo[cg * 8 + 4]);
-    const float4 b0 = *reinterpret_cast<const float4*>(&sCo[COUT + cg * 8]);
-    const float4 b1 = *reinterpret_cast<const float4*>(&sCo[COUT + cg * 8 + 4]);
-    const float ca[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-    const float cb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-    E8 o8;
-    uint32_t mb = 0u;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float z = (float)y8[e] * ca[e] + cb[e];
-      if (MODE == 1) z += (float)__builtin_bit_cast(E8, rq[j])[e];
-      o8[e] = (E)fmaxf(z, 0.f);
-      mb |= ((float)o8[e] > 0.f ? 1u : 0u) << e;
-    }
-    *reinterpret_cast<u32x4*>(&p.out[base + (size_t)c * 8]) = __builtin_bit_cast(u32x4, o8);
-    if (p.rmask) p.rmask[(size_t)n * WR_P * 12 + c] = (uint8_t)mb;
-  }
-}
-
-template <typename E, int MODE>
-__device__ __forceinline__ void wr_memory(const FwdParams<E>& p, E* sX, const E* sY, const float* sGB,
-                                          const float* sSt, float* sCo, int lane, int cnt) {
-  wr_stage(p, sX, 0, lane);
-  if (cnt > 1) wr_stage(p, sX, 1, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  lds_barrier();  // BAR_0
-  for (int k = 0; k < cnt; ++k) {
-    if (k >= 1) {  // between BAR_2(k-1) and BAR_1(k): tile k+1 into the buffer conv k-1 freed
-      if (k + 1 < cnt) wr_stage(p, sX, k + 1, lane);
-      wr_epilogue<E, MODE>(p, sY, sGB, sSt, sCo, k - 1, lane, k + 1 < cnt);
-    }
-    lds_barrier();  // BAR_1(k)
-    lds_barrier();  // BAR_2(k)
-  }
-  wr_epilogue<E, MODE>(p, sY, sGB, sSt, sCo, cnt - 1, lane, false);
-}
-
-template <typename E, int MODE>
-__global__ __launch_bounds__(256, 1) void k_conv_gn_fwd_wr(FwdParams<E> p) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  E* sX = reinterpret_cast<E*>(smem);                              // [2][257][104]
-  E* sY = sX + 2 * WR_XB;                                          // [256][96]
-  float* sGB = reinterpret_cast<float*>(sY + WR_P * COUT);         // gamma | beta
-  float* sSt = sGB + 2 * COUT;                                     // [6][2] mean, rstd
-  float* sCo = sSt + 2 * NGRP;                                     // [2][96] scale, shift (memory wave)
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int cnt = ((int)p.N - 1 - (int)blockIdx.x) / (int)gridDim.x + 1;  // grid <= N: cnt >= 1
-  if (tid < 2 * 13)  // the zero row (pixel 256) of both buffers; never overwritten
-    *reinterpret_cast<u32x4*>(&sX[(tid / 13) * WR_XB + WR_P * WR_CINP + (tid % 13) * 8]) = u32x4{0u, 0u, 0u, 0u};
-  for (int i = tid; i < COUT; i += 256) {
-    sGB[i] = p.gamma[i];
-    sGB[COUT + i] = p.beta[i];
-  }
-  if (wave < 3) wr_compute<E>(p, sX, sY, sSt, wave, lane, cnt);
-  else wr_memory<E, MODE>(p, sX, sY, sGB, sSt, sCo, lane, cnt);
-}
-
-template <typename E, int MODE>
-int launch_fwd_wr(const FwdParams<E>& p, hipStream_t s) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k_conv_gn_fwd_wr<E, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    attr_set = true;
-  }
-  const int grid = p.N < num_cus() ? p.N : num_cus();
-  hipLaunchKernelGGL((k_conv_gn_fwd_wr<E, MODE>), dim3(grid), dim3(256), WR_LDS, s, p);
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) {
-    snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd launch: %s", hipGetErrorString(e));
-    return MS_EHIP;
-  }
-  return MS_OK;
-}
-
 template <typename E, int CIN, int NPT, bool FULL>
 int launch_fwd(const FwdParams<E>& p, hipStream_t s) {
   constexpr int CINP = cinp<CIN>();
@@ -691,20 +406,9 @@ int launch_fwd(const FwdParams<E>& p, hipStream_t s) {
   return MS_OK;
 }
 
-int g_fwd_impl = MC_FWD_AUTO;  // mc_set_fwd_impl (measurement / A-B only)
-
 template <typename E, int CIN>
 int dispatch_fwd(const FwdParams<E>& p, hipStream_t s) {
   const int P = p.H * p.W;
-  if constexpr (CIN == 96) {
-    // weight-resident kernel: 16x16 boards, not residual and dropout together (never both in
-    // CNNResidualPolicy: dropout follows a block's first conv, the residual its second)
-    if (g_fwd_impl == MC_FWD_AUTO && p.H == 16 && p.W == 16 && !(p.res && p.dmask)) {
-      if (p.res) return launch_fwd_wr<E, 1>(p, s);
-      if (p.dmask) return launch_fwd_wr<E, 2>(p, s);
-      return launch_fwd_wr<E, 0>(p, s);
-    }
-  }
   const int tiles = (P + 31) / 32;
   const int npt = (tiles + WAVES - 1) / WAVES;
   if (P == 256) return launch_fwd<E, CIN, 2, true>(p, s);
@@ -759,15 +463,6 @@ int run_fwd(const uint16_t* x, const uint16_t* w, const float* bias, const float
 extern "C" {
 
 const char* mc_last_error(void) { return g_err; }
-
-int mc_set_fwd_impl(int32_t impl) {
-  if (impl != MC_FWD_AUTO && impl != MC_FWD_PER_SAMPLE) {
-    snprintf(g_err, sizeof g_err, "mc_set_fwd_impl: bad value %d", impl);
-    return MS_EINVAL;
-  }
-  g_fwd_impl = impl;
-  return MS_OK;
-}
 
 #ifdef MC_DIAG
 // diagnostics only (not in mscnn.h): per-workgroup phase cycle totals of the next forwards

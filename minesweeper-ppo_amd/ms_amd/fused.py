@@ -39,17 +39,6 @@ _vp, _i32, _f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_float
 _fwd = None
 
 
-FWD_IMPLS = {"auto": 0, "per_sample": 1}  # MC_FWD_AUTO / MC_FWD_PER_SAMPLE (include/mscnn.h)
-
-
-def set_fwd_impl(name: str) -> None:
-    """Measurement / A-B only: which forward kernel mc_conv_gn_fwd runs (process-wide).
-    "auto" (default): the weight-resident wave-specialised kernel on 16x16 boards with 96
-    input channels, the per-sample kernel otherwise; "per_sample": always the latter."""
-    f = _fn("mc_set_fwd_impl", [_i32])
-    _check(f(FWD_IMPLS[name]))
-
-
 def _check(rc):
     if rc != 0:
         lib = L.load()

@@ -17,6 +17,9 @@ for p in (ROOT, PKG_DIR, os.path.join(ROOT, "oracle")):
 # exact fp32 convolutions for the fp32 parity tests (ms_amd.exact_fp32_convs), set before MIOpen
 # runs anything; spawned test workers inherit it
 os.environ.setdefault("MIOPEN_DEBUG_CONV_WINOGRAD", "0")
+# the fp32 reference convolutions of the production-size parity tests run once per shape: MIOpen's
+# heuristic (immediate) find instead of an exhaustive search per new shape
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
 
 
 def pytest_configure(config):

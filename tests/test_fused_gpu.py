@@ -147,6 +147,8 @@ def test_conv_gn_bwd_matches_torch(gpu, H, W, cin, n, with_res, dt):
         assert _rel(dx, nhwc(dxr) + (add.float() if add is not None else 0)) < 1e-2
     if with_res:
         assert _rel(dz, nhwc(z.grad)) < 1e-2
+    if n > 1000:  # production sizes: the tight check above is the parity check (the loose one
+        return    # below only re-tests the ReLU-flip noise, at a large cost in fp32 convolutions)
     # loose: full fp32 recompute from x
     xq = xr.clone().requires_grad_(True)
     wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
@@ -200,49 +202,3 @@ def test_heads_match_torch(gpu, n, P, with_mine, dt):
     ref.update({"m" + k: v.grad for k, v in mine.named_parameters()} if with_mine else {})
     for k in ref:
         assert _rel(got[k], ref[k]) < 1e-2, (k, _rel(got[k], ref[k]))
-
-
-@pytest.mark.parametrize("n", [300, pytest.param(32768, id="c2-32768")])
-@pytest.mark.parametrize("dt", DT)
-def test_fwd_kernels_agree(gpu, n, dt):
-    """16x16 boards, 96 channels: the weight-resident wave-specialised forward (the default) and
-    the per-sample forward (mc_set_fwd_impl) compute the same layer: y bit-identical (same MFMA
-    accumulation order over taps and k steps), statistics within f32 summation-order noise,
-    outputs within one 16-bit rounding, ReLU bitmasks equal but for z ~ 0 ties."""
-    from ms_amd.fused import conv_gn_fwd, prep_weight, set_fwd_impl
-    torch.manual_seed(4)
-    P = 256
-    x = (torch.randn(n, P, 96, device=gpu) * 0.5).to(dt)
-    w = torch.randn(96, 96, 3, 3, device=gpu) * (1.0 / (3 * 96 ** 0.5))
-    b, g, be = torch.randn(96, device=gpu) * 0.1, 1 + 0.1 * torch.randn(96, device=gpu), 0.1 * torch.randn(96, device=gpu)
-    wt = prep_weight(w, 96, dt)
-    res = torch.randn(n, P, 96, device=gpu).to(dt)
-    dmask = (torch.rand(n, 96, device=gpu) > 0.05).float() / 0.95
-    try:
-        for kw in (dict(res=res), dict(dmask=dmask), {}):
-            outs = {}
-            for impl in ("per_sample", "auto"):
-                set_fwd_impl(impl)
-                outs[impl] = conv_gn_fwd(x, wt, b, g, be, 16, 16, want_mask=True, **kw)
-            (o_a, y_a, s_a, m_a), (o_p, y_p, s_p, m_p) = outs["auto"], outs["per_sample"]
-            assert torch.equal(y_a, y_p)
-            torch.testing.assert_close(s_a, s_p, rtol=1e-5, atol=1e-5)
-            torch.testing.assert_close(o_a.float(), o_p.float(), rtol=2e-2, atol=2e-2)
-            assert float((m_a != m_p).float().mean()) < 1e-3
-    finally:
-        set_fwd_impl("auto")
-
-
-@pytest.mark.parametrize("with_res", [False, True])
-@pytest.mark.parametrize("dt", DT)
-def test_per_sample_fwd_kernel_matches_torch(gpu, with_res, dt):
-    """The per-sample forward stays covered at 16x16 x 96 (the default dispatch takes the
-    weight-resident kernel there): the fp32-reference forward and backward checks above, run
-    with mc_set_fwd_impl(per_sample)."""
-    from ms_amd.fused import set_fwd_impl
-    set_fwd_impl("per_sample")
-    try:
-        test_conv_gn_fwd_matches_torch(gpu, 16, 16, 96, 300, with_res, dt)
-        test_conv_gn_bwd_matches_torch(gpu, 16, 16, 96, 300, with_res, dt)
-    finally:
-        set_fwd_impl("auto")

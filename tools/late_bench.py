@@ -1,5 +1,6 @@
-"""Cost of late-start resets (k_late, one serial wave over the step's done envs in env
-order, as the reference's single shared generator requires) on the tape + step loop.
+"""Cost of late-start resets on the tape + step loop: the shared generator (k_late, one serial
+wave over the step's done envs in env order, as the reference's single generator requires) and
+the keyed mode (k_late_keyed, one wave per resetting env, all at once; include/msenv.h).
 
     python tools/late_bench.py [--envs 4096] [--steps 200]
 """
@@ -21,9 +22,11 @@ ap.add_argument("--steps", type=int, default=200)
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 cfg = EnvConfig(H=16, W=16, mine_count=40)
-for name, late in [("no late start", None),
-                   ("late start p=0.5, 20-120 hidden", dict(prob=0.5, min_hidden=20, max_hidden=120)),
-                   ("late start p=1.0, 20-120 hidden", dict(prob=1.0, min_hidden=20, max_hidden=120))]:
+cases = [("no late start", None)]
+for rng in ("shared", "keyed"):
+    for p in (0.5, 1.0):
+        cases.append((f"{rng} late start p={p}, 20-120 hidden", dict(prob=p, min_hidden=20, max_hidden=120, rng=rng)))
+for name, late in cases:
     v = VecMinesweeper(a.envs, cfg, seed=0, late_start_cfg=late, late_start_seed=1, device=dev)
     v.reset()
     dones = 0
@@ -36,5 +39,5 @@ for name, late in [("no late start", None),
         dones += d
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / a.steps
-    print(f"{name:34s}: {el * 1e6:7.1f} us/step (eager tape + step), "
+    print(f"{name:40s}: {el * 1e6:7.1f} us/step (eager tape + step), "
           f"{a.envs / el / 1e6:7.1f} M env-steps/s, {float(dones.sum()) / a.steps:6.1f} resets/step", flush=True)

@@ -30,7 +30,8 @@ int ms_event_elapsed_ms(void* start_event, void* stop_event, float* ms);
 int ms_event_destroy(void* event);
 
 /* libmsenv_diag.so only: per-env s_memtime/s_memrealtime stamps, device
- * u64[env_count][8] (NULL disables). Ignored by the production build. */
+ * u64[env_count][16] (slots 0-5 phases, 6-7 realtime, 8-14 placement sub-phases; NULL
+ * disables). Ignored by the production build. */
 int ms_set_diag(ms_handle* h, uint64_t* stamps);
 
 #ifdef __cplusplus

@@ -534,9 +534,22 @@ __device__ __forceinline__ uint32_t bperm(uint32_t v, int src_lane) {
 // fixpoint; collision chains are short, ~2-4 rounds). Set membership uses a
 // round-tagged LDS table indexed by cell. Returns false on a Lemire rejection
 // (caller falls back to place_serial), leaving rng untouched.
+// MS_DIAG builds: sub-phase stamps of a placement (diag slots 8..13 of the env)
+#ifdef MS_DIAG
+#define PSTAMP(k)                                                  \
+  do {                                                             \
+    if (dg && lane == 0) dg[(k)] = __builtin_amdgcn_s_memtime();    \
+  } while (0)
+#else
+#define PSTAMP(k) do { } while (0)
+#endif
+
 template <int H_, int W_>
 __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, int K, const uint64_t (&J)[4],
-                               uint32_t* tab, uint64_t* srow, const Geo<H_, W_>& g, int lane) {
+                               uint32_t* tab, uint64_t* srow, const Geo<H_, W_>& g, int lane,
+                               uint64_t* dg = nullptr) {
+  (void)dg;
+  PSTAMP(8);
   const int A = g.A(), W = g.W;
   const int pop = F.pop;
   const int z0 = (pop == K) ? 1 : 0;
@@ -550,6 +563,7 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
   const Out o0 = jump_out(rng.hi, rng.lo, J[0], J[1], ci_hi, ci_lo);
   Out o1 = o0;
   if (n_out > 64) o1 = jump_out(readlane64(o0.sh, 63), readlane64(o0.sl, 63), J[0], J[1], ci_hi, ci_lo);
+  PSTAMP(9);
   // Lemire rejection test of every consumed draw (draw p of output q, half hf)
   bool rej = false;
   if (h0 && D > 0) {
@@ -571,6 +585,7 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
     }
   }
   if (__ballot(rej) != 0ull) return false;
+  PSTAMP(10);
   // Floyd candidates: lane owns iterations i = lane + 64 s
   int cand[2], alt[2], sel[2];
   bool valid[2];
@@ -595,7 +610,11 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
   }
   for (int c = lane; c < A; c += kWave) tab[c] = 0u;
   wave_sync();
+  PSTAMP(11);
   for (uint32_t round = 1; round <= (uint32_t)K + 1; ++round) {
+#ifdef MS_DIAG
+    if (dg && lane == 0) dg[14] = round;
+#endif
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
       if (valid[s2]) atomicMax(&tab[sel[s2]], (round << 16) | (0xFFFFu - (uint32_t)(lane + 64 * s2)));
@@ -614,6 +633,7 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
     wave_sync();
     if (__ballot(changed) == 0ull) break;
   }
+  PSTAMP(12);
   srow[lane] = 0ull;
   wave_sync();
 #pragma unroll
@@ -634,6 +654,7 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
     rng.uinteger = readlane32((uint32_t)(ol.x >> 32), lastq & 63);
   }
   if (D > 0) rng.has32 = (uint32_t)(rem & 1);
+  PSTAMP(13);
   return true;
 }
 
@@ -645,9 +666,9 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
 #define STAMP(k)                                                              \
   do {                                                                        \
     if (p.diag && lane == 0) {                                                \
-      p.diag[env * 8 + (k)] = __builtin_amdgcn_s_memtime();                   \
-      if ((k) == 0) p.diag[env * 8 + 6] = __builtin_amdgcn_s_memrealtime();   \
-      if ((k) == 5) p.diag[env * 8 + 7] = __builtin_amdgcn_s_memrealtime();   \
+      p.diag[env * 16 + (k)] = __builtin_amdgcn_s_memtime();                  \
+      if ((k) == 0) p.diag[env * 16 + 6] = __builtin_amdgcn_s_memrealtime();  \
+      if ((k) == 5) p.diag[env * 16 + 7] = __builtin_amdgcn_s_memrealtime();  \
     }                                                                         \
   } while (0)
 #else
@@ -678,7 +699,12 @@ __device__ __forceinline__ void board_click(Pcg& rng, uint64_t& mine, uint64_t& 
       bool ok = false;
       if (!(p.dbg_flags & MS_DBG_FORCE_SERIAL_PLACEMENT)) {
         if (p.K >= 1 && p.K <= 128 && !(p.dbg_flags & MS_DBG_FORCE_CHAIN_PLACEMENT))
+#ifdef MS_DIAG
+          ok = place_fixpoint(rng, mine, F, p.K, J, sTab, sR, g, lane,
+                              (p.diag && env >= 0) ? p.diag + env * 16 : nullptr);
+#else
           ok = place_fixpoint(rng, mine, F, p.K, J, sTab, sR, g, lane);
+#endif
         else
           ok = place_parallel(rng, mine, F, p.K, J, g, lane);
       }

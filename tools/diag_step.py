@@ -25,7 +25,7 @@ H, W, K = (int(x) for x in args.board.split("x"))
 from ms_amd import EnvConfig, VecMinesweeper, _lib as L  # noqa: E402
 
 v = VecMinesweeper(args.envs, EnvConfig(H=H, W=W, mine_count=K), seed=0)
-stamps = torch.zeros((args.envs, 8), dtype=torch.int64, device="cuda")
+stamps = torch.zeros((args.envs, 16), dtype=torch.int64, device="cuda")
 v.reset()
 for t in range(30):
     v.step(v.tape_actions(t, args.tape))
@@ -33,6 +33,7 @@ L.check(v._lib.ms_set_diag(v._h, stamps.data_ptr()))
 rows = []
 for t in range(30, 30 + args.steps):
     a = v.tape_actions(t, args.tape)
+    stamps.zero_()
     torch.cuda.synchronize()
     v.step(a)
     torch.cuda.synchronize()
@@ -46,6 +47,18 @@ for i, n in enumerate(names):
     print(f"  {n:14s} mean {col.mean():9.0f}  p50 {np.median(col):9.0f}  p99 {np.percentile(col, 99):9.0f}  max {col.max():9.0f}")
 tot = S[:, 5] - S[:, 0]
 print(f"  {'total':14s} mean {tot.mean():9.0f}  p50 {np.median(tot):9.0f}  p99 {np.percentile(tot, 99):9.0f}  max {tot.max():9.0f}")
+# placement sub-phases (slots 8..13; 14 = fixpoint rounds) of the boards that placed this step
+pl = S[:, 13] > S[:, 8]
+if pl.any():
+    P_ = S[pl]
+    sub = np.diff(P_[:, 8:14], axis=1).astype(np.float64)
+    sn = ["jump-ahead", "lemire", "candidates+clear", "fixpoint", "rows+state"]
+    print(f"  placement sub-phases over {pl.sum()} placements (of {len(S)} board steps):")
+    for i, n in enumerate(sn):
+        print(f"    {n:16s} mean {sub[:, i].mean():8.0f}  p50 {np.median(sub[:, i]):8.0f}  p99 {np.percentile(sub[:, i], 99):8.0f}")
+    print(f"    fixpoint rounds mean {P_[:, 14].mean():.2f} max {P_[:, 14].max()}")
+    pt = (P_[:, 2] - P_[:, 1]).astype(np.float64)
+    print(f"    whole placement phase of placing boards: mean {pt.mean():.0f} p50 {np.median(pt):.0f} p99 {np.percentile(pt, 99):.0f}")
 # realtime (100 MHz): spread of wave starts/ends within one launch
 for k in range(args.steps):
     blk = rows[k]

@@ -182,6 +182,10 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   return z ^ (z >> 31);
 }
 
+#ifndef MS_EXP
+#define MS_EXP 0
+#endif
+
 // ---------------------------------------------------------------------------
 // Board geometry: compile-time for the benchmark shapes, runtime otherwise.
 // Rows are packed RPW = floor(64/W) rows per u64 word (no row straddles a
@@ -695,6 +699,14 @@ __device__ __forceinline__ void board_click(Pcg& rng, uint64_t& mine, uint64_t& 
   const bool cell_rev = (readlane64(rev, ar) >> ac) & 1ull;
   if (!cell_rev) {
     if (!fc) {
+#if MS_EXP == 1  // timing experiment only: a fixed mine pattern instead of the placement
+      mine = lane < H ? ((0x0101010101010101ull << (lane & 7)) & rowmask) : 0ull;
+      if (lane >= ar - 1 && lane <= ar + 1) mine &= ~(7ull << (ac > 0 ? ac - 1 : 0));
+      fc = true;
+      mines_changed = true;
+    }
+    if (false) {
+#endif
       const Forbid F = make_forbid(cell, ar, ac, p.K, p.guarantee != 0, g);
       bool ok = false;
       if (!(p.dbg_flags & MS_DBG_FORCE_SERIAL_PLACEMENT)) {

@@ -182,10 +182,6 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   return z ^ (z >> 31);
 }
 
-#ifndef MS_EXP
-#define MS_EXP 0
-#endif
-
 // ---------------------------------------------------------------------------
 // Board geometry: compile-time for the benchmark shapes, runtime otherwise.
 // Rows are packed RPW = floor(64/W) rows per u64 word (no row straddles a
@@ -612,35 +608,9 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
     alt[s2] = map_allowed(j, F.f, F.m);
     sel[s2] = cand[s2];
   }
-  PSTAMP(11);
-  if (A <= 256) {
-    // Boards of up to 256 cells: Floyd's sequential rule as a chain on a wave-uniform
-    // 256-bit set of chosen cells (scalar registers): per iteration one readlane of the
-    // candidate, a bit test, (on a hit) one readlane of j, a bit set. ~10 scalar
-    // instructions per mine instead of the LDS table's atomic rounds.
-    uint64_t w0 = 0ull, w1 = 0ull, w2 = 0ull, w3 = 0ull;
-    for (int i = 0; i < K; ++i) {
-      const int s2 = i >> 6, li = i & 63;
-      int t = (int)readlane32((uint32_t)(s2 ? cand[1] : cand[0]), li);
-      const uint64_t wt = (t >> 6) == 0 ? w0 : ((t >> 6) == 1 ? w1 : ((t >> 6) == 2 ? w2 : w3));
-      if ((wt >> (t & 63)) & 1ull) t = (int)readlane32((uint32_t)(s2 ? alt[1] : alt[0]), li);
-      const uint64_t bit = 1ull << (t & 63);
-      const int wi = t >> 6;
-      w0 |= wi == 0 ? bit : 0ull;
-      w1 |= wi == 1 ? bit : 0ull;
-      w2 |= wi == 2 ? bit : 0ull;
-      w3 |= wi == 3 ? bit : 0ull;
-    }
-    PSTAMP(12);
-    // row r of the board: bits [r*W, r*W + W) of the set (a row may straddle two words)
-    const int c0 = lane * W, wi = c0 >> 6, sh = c0 & 63;
-    const uint64_t lo = wi == 0 ? w0 : (wi == 1 ? w1 : (wi == 2 ? w2 : w3));
-    const uint64_t hi = wi == 0 ? w1 : (wi == 1 ? w2 : (wi == 2 ? w3 : 0ull));
-    const uint64_t row = (lo >> sh) | (sh ? hi << (64 - sh) : 0ull);
-    mine_out = lane < g.H ? row & g.rowmask() : 0ull;
-  } else {
   for (int c = lane; c < A; c += kWave) tab[c] = 0u;
   wave_sync();
+  PSTAMP(11);
   for (uint32_t round = 1; round <= (uint32_t)K + 1; ++round) {
 #ifdef MS_DIAG
     if (dg && lane == 0) dg[14] = round;
@@ -675,7 +645,6 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
   wave_sync();
   mine_out = lane < g.H ? srow[lane] : 0ull;
   wave_sync();
-  }
   // RNG state after the D draws
   if (n_out > 0) {
     const int lastq = n_out - 1;
@@ -726,14 +695,6 @@ __device__ __forceinline__ void board_click(Pcg& rng, uint64_t& mine, uint64_t& 
   const bool cell_rev = (readlane64(rev, ar) >> ac) & 1ull;
   if (!cell_rev) {
     if (!fc) {
-#if MS_EXP == 1  // timing experiment only: a fixed mine pattern instead of the placement
-      mine = lane < H ? ((0x0101010101010101ull << (lane & 7)) & rowmask) : 0ull;
-      if (lane >= ar - 1 && lane <= ar + 1) mine &= ~(7ull << (ac > 0 ? ac - 1 : 0));
-      fc = true;
-      mines_changed = true;
-    }
-    if (false) {
-#endif
       const Forbid F = make_forbid(cell, ar, ac, p.K, p.guarantee != 0, g);
       bool ok = false;
       if (!(p.dbg_flags & MS_DBG_FORCE_SERIAL_PLACEMENT)) {

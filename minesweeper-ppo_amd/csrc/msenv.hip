@@ -608,27 +608,9 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
     alt[s2] = map_allowed(j, F.f, F.m);
     sel[s2] = cand[s2];
   }
-  PSTAMP(11);
-  if (K <= 16) {
-    // Few mines (9x9x10, 8x8x10, ...): each round broadcasts the K selections and lane i
-    // tests its candidate against those of the lanes before it; no LDS table, no atomics
-    for (uint32_t round = 1; round <= (uint32_t)K + 1; ++round) {
-#ifdef MS_DIAG
-      if (dg && lane == 0) dg[14] = round;
-#endif
-      bool coll = false;
-      for (int k = 0; k < K; ++k) {
-        const int v = (int)readlane32((uint32_t)sel[0], k);
-        coll |= (lane > k) && (v == cand[0]);
-      }
-      const int nv = coll ? alt[0] : cand[0];
-      const bool changed = valid[0] && nv != sel[0];
-      if (valid[0]) sel[0] = nv;
-      if (__ballot(changed) == 0ull) break;
-    }
-  } else {
   for (int c = lane; c < A; c += kWave) tab[c] = 0u;
   wave_sync();
+  PSTAMP(11);
   for (uint32_t round = 1; round <= (uint32_t)K + 1; ++round) {
 #ifdef MS_DIAG
     if (dg && lane == 0) dg[14] = round;
@@ -650,7 +632,6 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
     }
     wave_sync();
     if (__ballot(changed) == 0ull) break;
-  }
   }
   PSTAMP(12);
   srow[lane] = 0ull;

@@ -76,11 +76,9 @@ struct FwdParams {
 template <int CIN>
 constexpr int cinp() { return CIN + 8; }  // +16 B per pixel row: conflict-free ds_read_b128
 
-constexpr int COUTP = COUT + 8;  // y staging row stride: conflict-free pair stores and 16-B reads
-
 template <int CIN>
 __host__ __device__ inline int region0_elems(int H, int W) {
-  const int a = (H * W + 1) * cinp<CIN>(), b = H * W * COUTP;
+  const int a = (H * W + 1) * cinp<CIN>(), b = H * W * COUT;
   return ((a > b ? a : b) + 7) & ~7;
 }
 
@@ -138,7 +136,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
   E* sO = sX;
   E* sW = sX + region0_elems<CIN>(H, W);
   float* sRed = reinterpret_cast<float*>(sW + COUT * CINP);
-  float* sGB = sRed + 2 * WAVES * NGRP;  // [gamma | beta]
+  float* sGB = sRed + WAVES * NGRP;  // [gamma | beta]
   float* sAB = sGB + 2 * COUT;        // per sample: [scale | shift | dropout scale]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
@@ -241,7 +239,6 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
     float gmean[NGRP], grstd[NGRP];
     const float inv_cnt = 1.0f / (16.0f * (float)P);
     for (int pass = 0; pass < 2; ++pass) {
-      float* sRp = sRed + pass * WAVES * NGRP;  // one buffer per pass: no barrier to reuse it
       float part[3];
 #pragma unroll
       for (int ct = 0; ct < 3; ++ct) {
@@ -270,8 +267,8 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
       if (lane == 0) {
 #pragma unroll
         for (int ct = 0; ct < 3; ++ct) {
-          sRp[wave * NGRP + 2 * ct] = gs[ct][0];
-          sRp[wave * NGRP + 2 * ct + 1] = gs[ct][1];
+          sRed[wave * NGRP + 2 * ct] = gs[ct][0];
+          sRed[wave * NGRP + 2 * ct + 1] = gs[ct][1];
         }
       }
       __syncthreads();
@@ -279,12 +276,11 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
       for (int g = 0; g < NGRP; ++g) {
         float tot = 0.f;
 #pragma unroll
-        for (int w = 0; w < WAVES; ++w) tot += sRp[w * NGRP + g];
+        for (int w = 0; w < WAVES; ++w) tot += sRed[w * NGRP + g];
         if (pass == 0) gmean[g] = tot * inv_cnt;
         else grstd[g] = rsqrtf(tot * inv_cnt + p.eps);
       }
-      // (no trailing barrier: the next write of this pass's buffer is a sample later, behind
-      // the taps' barriers)
+      __syncthreads();  // sRed reused by the next pass
     }
     FSTAMP(2);  // GroupNorm statistics
     if (p.stats && tid < NGRP) {
@@ -301,12 +297,12 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
 #pragma unroll
     for (int ct = 0; ct < 3; ++ct)
 #pragma unroll
-      for (int t = 0; t < NPT; ++t) {
-        float v[16];
+      for (int t = 0; t < NPT; ++t)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = acc[t][ct][i] + biasv[ct];
-        stage_tile_pairs(sO, COUTP, (wave * NPT + t) * 32, ct * 32, v, P, l32, hh);
-      }
+        for (int i = 0; i < 16; ++i) {
+          const int px = (wave * NPT + t) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          if (FULL || px < P) sO[px * COUT + ct * 32 + l32] = (E)(acc[t][ct][i] + biasv[ct]);
+        }
     FSTAMP(3);  // y -> LDS
     if (tid < COUT) {  // z = y * scale + shift (+ res), then ReLU, then * dropout scale
       const int g = tid >> 4;
@@ -357,8 +353,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
       }
       if ((FULL && k < NEC) || c < P * (COUT / 8)) {
         const size_t o = (size_t)n * P * COUT + (size_t)c * 8;
-        const int opx = c / (COUT / 8);
-        const u32x4 yv = *reinterpret_cast<const u32x4*>(&sO[opx * COUTP + (c - opx * (COUT / 8)) * 8]);
+        const u32x4 yv = *reinterpret_cast<const u32x4*>(&sO[c * 8]);
         if (p.ysave) *reinterpret_cast<u32x4*>(&p.ysave[o]) = yv;
         const E8 y8 = __builtin_bit_cast(E8, yv);
         const E8 r8 = __builtin_bit_cast(E8, rq[k % RB]);
@@ -387,7 +382,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
 template <typename E, int CIN, int NPT, bool FULL>
 int launch_fwd(const FwdParams<E>& p, hipStream_t s) {
   constexpr int CINP = cinp<CIN>();
-  const size_t lds = (size_t)region0_elems<CIN>(p.H, p.W) * 2 + (size_t)COUT * CINP * 2 + 2 * WAVES * NGRP * 4 +
+  const size_t lds = (size_t)region0_elems<CIN>(p.H, p.W) * 2 + (size_t)COUT * CINP * 2 + WAVES * NGRP * 4 +
                      5 * COUT * 4;
   if (lds > 160 * 1024) {
     snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd: board %dx%d needs %zu B LDS", p.H, p.W, lds);

@@ -68,7 +68,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
   typedef typename EV<E>::v8 E8;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int H = p.H, W = p.W, P = H * W;
-  E* sD = reinterpret_cast<E*>(smem);  // [P+1][DCP] (row P = 0); later [P][DCP] dx staging
+  E* sD = reinterpret_cast<E*>(smem);  // [P+1][DCP] (row P = 0); later [P][96] dx staging
   float* sRed = reinterpret_cast<float*>(smem + dtile_bytes(P));
   E* sW = reinterpret_cast<E*>(sRed);  // W^T[tap] as [ci][DCP]
   float* sCo = reinterpret_cast<float*>(smem + dtile_bytes(P) + red_bytes());  // [3][96]
@@ -316,16 +316,16 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
         __syncthreads();
       }
     }
-    // ---------------- epilogue: dx (+ addend) via a [P][DCP] staging image ----------------
+    // ---------------- epilogue: dx (+ addend) via a [P][96] staging image ----------------
 #pragma unroll
     for (int t = 0; t < NPT; ++t)
 #pragma unroll
-      for (int ct = 0; ct < 3; ++ct) {
-        float v[16];
+      for (int ct = 0; ct < 3; ++ct)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = acc[t][ct][i];
-        stage_tile_pairs(sD, DCP, (wave * NPT + t) * 32, ct * 32, v, P, l32, hh);
-      }
+        for (int i = 0; i < 16; ++i) {
+          const int px = (wave * NPT + t) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          if (px < P) sD[px * COUT + ct * 32 + l32] = (E)acc[t][ct][i];
+        }
     __syncthreads();
     if (gact) {
       u32x4 ad[NCH];  // all addend loads in flight before the first dependent store
@@ -339,7 +339,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
       for (int i = 0; i < NCH; ++i) {
         const int px = pg + PG * i;
         if (px < P) {
-          const E8 a8 = __builtin_bit_cast(E8, *reinterpret_cast<const u32x4*>(&sD[px * DCP + c8 * 8]));
+          const E8 a8 = __builtin_bit_cast(E8, *reinterpret_cast<const u32x4*>(&sD[px * COUT + c8 * 8]));
           const E8 r8 = __builtin_bit_cast(E8, ad[i]);
           E8 s8;
 #pragma unroll

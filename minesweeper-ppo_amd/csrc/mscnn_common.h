@@ -98,30 +98,6 @@ __device__ __forceinline__ f16x8 cat8(f16x4 lo, f16x4 hi) {
   return f16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-// Stages an MFMA 32x32 accumulator tile (lane l32 = channel col0 + l32, register i = row
-// (i & 3) + 8 (i >> 2) + 4 hh) into a row-major 16-bit LDS image img[row][stride] as 4-byte
-// pairs: registers i and i ^ 1 are rows r and r + 1; a lane-pair swap (DPP quad_perm
-// [1,0,3,2]) gives the even lane channels (c, c+1) of row r and the odd lane those of row
-// r + 1. One ds_write_b32 per two values and no two lanes on one dword (a b16 store per
-// value puts two lanes on each dword). Rows >= nrows are not written.
-template <typename E>
-__device__ __forceinline__ void stage_tile_pairs(E* img, int stride, int row0, int col0, const float (&v)[16],
-                                                 int nrows, int l32, int hh) {
-  const bool odd = l32 & 1;
-  const int c = col0 + (l32 & ~1);
-#pragma unroll
-  for (int i = 0; i < 16; i += 2) {
-    const float v0 = v[i], v1 = v[i + 1];
-    const float x = odd ? v0 : v1;
-    const float y = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0xB1, 0xf, 0xf, false));
-    const float lo = odd ? y : v0, hi = odd ? v1 : y;
-    const int r = row0 + (i & 3) + 8 * (i >> 2) + 4 * hh + (odd ? 1 : 0);
-    typedef E E2 __attribute__((ext_vector_type(2)));
-    const E2 pk = E2{(E)lo, (E)hi};
-    if (r < nrows) *reinterpret_cast<uint32_t*>(&img[r * stride + c]) = __builtin_bit_cast(uint32_t, pk);
-  }
-}
-
 // the dtype argument of the mscnn.h entry points
 enum { MC_DT_BF16 = 0, MC_DT_F16 = 1 };
 

@@ -6,7 +6,8 @@ can be checked against profiles/.
 
 k_step: mean dispatch duration of the config's grid (one 64-lane wave per env: grid
 threads = 64 * envs) -> algorithmic bytes / duration. k_run: the config's dispatches
-minus the first (the untimed warm-up launch), summed and divided by the timed steps.
+minus the first (the untimed warm-up launch), summed and divided by the timed steps (the
+multistep record's timed_steps: bench.py times max(--steps, --min-timed-steps) of them).
 """
 import argparse
 import csv
@@ -70,7 +71,7 @@ for p in pts:
     kr = sorted(disp.get(("k_run", hw, grid), []))
     if ms and len(kr) > 1:
         timed = kr[1:]
-        steps = line["steps"]
+        steps = ms.get("timed_steps", line["steps"])
         per_step_ms = sum(d for _, d in timed) / steps / 1e6
         mrl = ms["roofline"]
         tf = per_launch / (per_step_ms * 1e-3) / 1e9 / mrl["peak"]

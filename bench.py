@@ -72,6 +72,8 @@ def parse():
                     help="the captured K-step graph is replayed until at least this many steps are timed "
                          "(SURVEY.md §8d: >= 1,000 timed steps)")
     ap.add_argument("--diag-no-obs", action="store_true", help="diagnostic: skip obs/mask outputs")
+    ap.add_argument("--env-debug-flags", type=int, default=0,
+                    help="diagnostic A/B only: msenv_debug.h MS_DBG_* flags of the env handles (4: no lane packing)")
     ap.add_argument("--graph", type=int, default=1, help="capture the timed steps in a HIP graph")
     ap.add_argument("--ppo-updates", type=int, default=2,
                     help="timed combined rollout+GAE+PPO updates (0 disables; +1 untimed warm-up)")
@@ -346,6 +348,8 @@ def env_bench(args, world, rank, dev, H, W, K, n_local, multistep=True):
     vec = VecMinesweeper(n_total, EnvConfig(H=H, W=W, mine_count=K), seed=args.seed, device=dev,
                          shard=(rank, world))
     assert vec.num_envs == n_local
+    if args.env_debug_flags:
+        vec.set_debug_flags(args.env_debug_flags)
     A = H * W
     # obs/mask go to a ring of R slots holding > 512 MiB (2x the 256 MiB Infinity Cache), as a
     # rollout buffer would: a single re-written 44 MB buffer stays cache-resident and its

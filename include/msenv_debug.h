@@ -16,6 +16,8 @@ extern "C" {
 /* debug flags */
 #define MS_DBG_FORCE_SERIAL_PLACEMENT 1u /* serial reference-order PCG draws + Floyd chain */
 #define MS_DBG_FORCE_CHAIN_PLACEMENT 2u  /* jump-ahead draws + serial Floyd chain (K > 128 path) */
+#define MS_DBG_ONE_BOARD_PER_WAVE 4u     /* ms_step: k_step (one board per wave) even where the
+                                            lane-packed k_step_packed applies (9x9, 8x8, K<=16) */
 
 int ms_set_debug_flags(ms_handle* h, uint32_t flags);
 

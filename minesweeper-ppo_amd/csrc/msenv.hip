@@ -882,6 +882,406 @@ __global__ __launch_bounds__(64 * EPW) void k_step(KParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// ms_step, lane-packed: four boards per wave for small boards (H <= 16, A <= 128,
+// 1 <= K <= 16; the 9x9x10 and 8x8x10 benchmark shapes). Board b of the wave lives
+// in DPP row b (lanes 16b..16b+15); lane 16b+r holds row r as a W-bit mask. Vertical
+// neighbours are row_shr/row_shl:1 with bound_ctrl, which stop at the board edge;
+// board sums are row_ror adds; a board-wide predicate is the board's 16 bits of a
+// wave ballot; and every per-board scalar (PCG64 state, click, step count) is a VGPR
+// that is uniform across the board's 16 lanes. The 4 boards' obs are one contiguous
+// 40*A-float span, written as full 1 KiB float4 wave stores from a per-cell plane-bit
+// table in this wave's LDS (wave-local: no workgroup barrier). A 9x9 board fills 9 of
+// 64 lanes in k_step; here 36 of 64, with a quarter of the waves.
+// ---------------------------------------------------------------------------
+constexpr int kPackBoards = 4;  // boards per wave
+
+__device__ __forceinline__ uint32_t row_shr1(uint32_t v) { return dpp32<0x111>(v); }  // r <- r-1; r=0 <- 0
+__device__ __forceinline__ uint32_t row_shl1(uint32_t v) { return dpp32<0x101>(v); }  // r <- r+1; r=15 <- 0
+// sum over the board's 16 lanes, result in each of them (row_ror:8,4,2,1)
+__device__ __forceinline__ uint32_t board_sum(uint32_t v) {
+  v += dpp32<0x128>(v);
+  v += dpp32<0x124>(v);
+  v += dpp32<0x122>(v);
+  v += dpp32<0x121>(v);
+  return v;
+}
+__device__ __forceinline__ bool board_any(bool v, int lane) {
+  return ((__ballot(v) >> (lane & 48)) & 0xffffull) != 0ull;
+}
+__device__ __forceinline__ uint32_t board_read(uint32_t v, int lane, int r) {  // v of lane 16b + r
+  return bperm(v, (lane & 48) | (r & 15));
+}
+__device__ __forceinline__ uint64_t board_read64(uint64_t v, int lane, int r) {
+  return ((uint64_t)board_read((uint32_t)(v >> 32), lane, r) << 32) | board_read((uint32_t)v, lane, r);
+}
+
+// row r (bits r*W .. r*W+W-1) of a 128-bit cell set
+template <int H_, int W_>
+__device__ __forceinline__ uint32_t set_row(uint64_t s0, uint64_t s1, int r, const Geo<H_, W_>& g) {
+  if (r >= g.H) return 0u;
+  const int s = r * g.W;
+  const uint64_t v = s >= 64 ? (s1 >> (s - 64)) : ((s0 >> s) | (s ? (s1 << (64 - s)) : 0ull));
+  return (uint32_t)(v & g.rowmask());
+}
+__device__ __forceinline__ bool set_has(uint64_t s0, uint64_t s1, uint32_t c) {
+  return (((c < 64u) ? s0 : s1) >> (c & 63u)) & 1ull;
+}
+__device__ __forceinline__ void set_add(uint64_t& s0, uint64_t& s1, uint32_t c) {
+  const uint64_t bit = 1ull << (c & 63u);
+  if (c < 64u) s0 |= bit;
+  else s1 |= bit;
+}
+
+// The forbidden cells of a placement (env.py:280-307) as a block: nr rows of nc cells from
+// cell base0 (the click's clipped 3x3 neighbourhood, or the click alone: nr = nc = 1).
+struct Block {
+  int base0, nr, nc, pop;
+};
+template <int H_, int W_>
+__device__ __forceinline__ Block make_block(int cell, int ar, int ac, int K, bool guarantee) {
+  Block B;
+  if (guarantee) {
+    const int r0 = ar > 0 ? ar - 1 : 0, r1 = ar < H_ - 1 ? ar + 1 : H_ - 1;
+    const int c0 = ac > 0 ? ac - 1 : 0, c1 = ac < W_ - 1 ? ac + 1 : W_ - 1;
+    B.base0 = r0 * W_ + c0;
+    B.nr = r1 - r0 + 1;
+    B.nc = c1 - c0 + 1;
+  } else {
+    B.base0 = cell;
+    B.nr = B.nc = 1;
+  }
+  B.pop = H_ * W_ - B.nr * B.nc;
+  if (B.pop < K) {  // env.py:303-307: relax to the clicked cell only
+    B.base0 = cell;
+    B.nr = B.nc = 1;
+    B.pop = H_ * W_ - 1;
+  }
+  return B;
+}
+// allowed index t -> cell (numpy's flatnonzero(~forbidden)[t], env.py:302), closed form:
+// past base0 the allowed cells come in gaps of W - nc between the block's row runs.
+template <int W_>
+__device__ __forceinline__ int map_block(int t, const Block& B) {
+  static_assert(W_ > 3, "a 3-wide block must leave a gap in every row");
+  if (t < B.base0) return t;
+  const int tp = t - B.base0;
+  const int q = B.nc == 3 ? tp / (W_ - 3) : (B.nc == 2 ? tp / (W_ - 2) : tp / (W_ - 1));
+  return B.base0 + tp + B.nc * (1 + (q < B.nr - 1 ? q : B.nr - 1));
+}
+
+// Placement of one packed board (same draws and result as place_fixpoint). The <= 16
+// PCG64 outputs come from one jump-ahead per lane (lane r: output r+1), and lane r owns
+// Floyd iteration r: j_r = pop-K+r, t_r = bounded draw in [0, j_r]. Floyd inserts t_r
+// unless it is already chosen, then j_r. Because the j are distinct and exceed every
+// earlier choice, "t_i already chosen" has a closed form: t_i equals an earlier t_k (which
+// is chosen either way), or equals j_k for the one k = t_i - (pop-K) < i whose own t_k
+// collided. Lane i gets the first from the board's 16 t values (one LDS broadcast read)
+// and resolves the second by following k (a bpermute per link; chains are short).
+// Mine rows are built with LDS ORs. Returns false on a Lemire rejection, leaving rng
+// untouched (the caller then runs place_serial_packed).
+template <int H_, int W_>
+__device__ bool place_packed(Pcg& rng, uint32_t& mine_out, const Block& B, int K, const uint64_t (&J)[4],
+                             uint32_t* sBuf, int lane) {
+  const int r = lane & 15;
+  const int pop = B.pop;
+  const int z0 = (pop == K) ? 1 : 0;
+  const int nF = K - z0;
+  const int D = nF + (K - 1);
+  const int h0 = rng.has32 ? 1 : 0;
+  const int rem = D - h0;
+  const int n_out = (rem + 1) >> 1;  // <= K <= 16
+  const uint64_t ci_lo = J[3] * rng.ilo;
+  const uint64_t ci_hi = __umul64hi(J[3], rng.ilo) + J[3] * rng.ihi + J[2] * rng.ilo;
+  const Out o = jump_out(rng.hi, rng.lo, J[0], J[1], ci_hi, ci_lo);
+  bool rej = false;
+  if (h0 && D > 0) {
+    const uint32_t bound = (nF > 0) ? (uint32_t)(pop - K + z0) : (uint32_t)(K - 1);
+    rej |= lemire_rejects((uint32_t)((uint64_t)rng.uinteger * (bound + 1u)), bound);
+  }
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    const int pidx = h0 + 2 * r + hf;
+    if (r < n_out && pidx < D) {
+      const uint32_t d = hf ? (uint32_t)(o.x >> 32) : (uint32_t)o.x;
+      const uint32_t bound = pidx < nF ? (uint32_t)(pop - K + z0 + pidx) : (uint32_t)(K - 1 - (pidx - nF));
+      rej |= lemire_rejects((uint32_t)((uint64_t)d * (bound + 1u)), bound);
+    }
+  }
+  if (board_any(rej, lane)) return false;
+  // lane r: Floyd iteration i = r (draw pidx = i - z0, from output (pidx - h0) / 2)
+  const int jr = pop - K + r;
+  const int pidx = r - z0;
+  const int idx = pidx - h0;
+  const uint32_t wl = board_read((uint32_t)o.x, lane, (idx >> 1) & 15);
+  const uint32_t wh = board_read((uint32_t)(o.x >> 32), lane, (idx >> 1) & 15);
+  uint32_t d = (idx & 1) ? wh : wl;
+  if (h0 && pidx == 0) d = rng.uinteger;
+  const uint32_t t = r >= K ? 0xffffffffu : (r >= z0 ? (uint32_t)(((uint64_t)d * (uint32_t)(jr + 1)) >> 32) : 0u);
+  sBuf[lane] = t;
+  wave_sync();
+  const uint4* tb = reinterpret_cast<const uint4*>(sBuf + (lane & 48));
+  const uint4 q0 = tb[0], q1 = tb[1], q2 = tb[2], q3 = tb[3];
+  const uint32_t tk[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                           q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+  bool dup = false;
+#pragma unroll
+  for (int k = 0; k < 15; ++k) dup |= (k < r) && tk[k] == t;
+  const int ks = (int)t - (pop - K);  // t == j_ks
+  const bool kv = r < K && ks >= 0 && ks < r;
+  bool col = dup;
+  while (true) {
+    // every lane of the board takes part: ds_bpermute returns 0 from an EXEC-disabled source
+    const uint32_t col_ks = board_read(col ? 1u : 0u, lane, ks);
+    const bool nc = dup || (kv && col_ks != 0u);
+    const bool changed = __ballot(nc != col) != 0ull;
+    col = nc;
+    if (!changed) break;
+  }
+  const int cell = map_block<W_>(col ? jr : (int)t, B);
+  wave_sync();
+  sBuf[lane] = 0u;
+  wave_sync();
+  if (r < K) atomicOr(&sBuf[(lane & 48) + cell / W_], 1u << (cell % W_));
+  wave_sync();
+  mine_out = r < H_ ? sBuf[lane] : 0u;
+  wave_sync();
+  if (n_out > 0) {
+    const int lq = n_out - 1;
+    rng.hi = board_read64(o.sh, lane, lq);
+    rng.lo = board_read64(o.sl, lane, lq);
+    rng.uinteger = board_read((uint32_t)(o.x >> 32), lane, lq);
+  }
+  if (D > 0) rng.has32 = (uint32_t)(rem & 1);
+  return true;
+}
+
+// Serial reference-order placement of one packed board: each lane of the board runs
+// the same draws on its copy of the board's state (the Lemire-rejection fallback).
+template <int H_, int W_>
+__device__ void place_serial_packed(Pcg& rng, uint32_t& mine_out, const Block& B, int K, const Geo<H_, W_>& g,
+                                    int lane) {
+  uint64_t s0 = 0ull, s1 = 0ull;
+  for (int j = B.pop - K; j < B.pop; ++j) {
+    uint32_t c = (uint32_t)map_block<W_>((int)pcg_bounded(rng, (uint32_t)j), B);
+    if (set_has(s0, s1, c)) c = (uint32_t)map_block<W_>(j, B);
+    set_add(s0, s1, c);
+  }
+  for (int i = K - 1; i >= 1; --i) (void)pcg_bounded(rng, (uint32_t)i);  // shuffle draws
+  mine_out = set_row(s0, s1, lane & 15, g);
+}
+
+template <int H_, int W_>
+constexpr bool packable() {
+  return H_ >= 1 && H_ <= 16 && W_ >= 1 && W_ <= 31 && H_ * W_ <= 128;
+}
+
+#ifdef MS_DIAG
+#define PKSTAMP(k)                                                            \
+  do {                                                                        \
+    if (p.diag && r == 0 && live) {                                           \
+      p.diag[env * 16 + (k)] = __builtin_amdgcn_s_memtime();                  \
+      if ((k) == 0) p.diag[env * 16 + 6] = __builtin_amdgcn_s_memrealtime();  \
+      if ((k) == 5) p.diag[env * 16 + 7] = __builtin_amdgcn_s_memrealtime();  \
+    }                                                                         \
+  } while (0)
+#else
+#define PKSTAMP(k) do { } while (0)
+#endif
+
+template <int H_, int W_, int WPG>
+__global__ __launch_bounds__(64 * WPG) void k_step_packed(KParams p) {
+  static_assert(packable<H_, W_>(), "packed board shape");
+  constexpr int A = H_ * W_;
+  constexpr int RPW = 64 / W_;
+  constexpr int NW = (H_ + RPW - 1) / RPW;
+  constexpr uint32_t ROWMASK = (1u << W_) - 1u;
+  __shared__ float4 sImg_all[WPG][kPackBoards * 10 * A / 4];  // the 4 boards' obs, as stored
+  __shared__ uint32_t sMask_all[WPG][(kPackBoards * A + 3) / 4];  // their action-mask bytes
+  __shared__ __attribute__((aligned(16))) uint32_t sRow_all[WPG][kWave];
+  const int lane = lane_id();
+  const int r = lane & 15;
+  const int wv = (WPG == 1) ? 0 : (int)rfl(threadIdx.x >> 6);
+  const int64_t env0 = ((int64_t)blockIdx.x * WPG + wv) * kPackBoards;
+  const bool wave_live = env0 < p.n;
+  const int64_t env_raw = env0 + (lane >> 4);
+  const bool live = env_raw < p.n;
+  const int64_t env = live ? env_raw : p.n - 1;  // a board past the end loads env n-1, stores nothing
+  float* sImg = reinterpret_cast<float*>(sImg_all[wv]);
+  uint8_t* sMask = reinterpret_cast<uint8_t*>(sMask_all[wv]);
+  uint32_t* sRow = sRow_all[wv];
+  const Geo<H_, W_> g(H_, W_);
+  PKSTAMP(0);
+
+  EnvMeta* mp = p.meta + env;
+  uint64_t* mwords = p.mine_words + env * NW;
+  uint64_t* rwords = p.rev_words + env * NW;
+  uint32_t mine = (uint32_t)load_row(mwords, g, r);
+  uint32_t rev = (uint32_t)load_row(rwords, g, r);
+  uint64_t J[4] = {0ull, 0ull, 0ull, 0ull};  // jump entry k = r+1 (a placement uses outputs 1..K)
+  if (r < p.K) {
+    const ulonglong2* e = reinterpret_cast<const ulonglong2*>(p.jump + 4 * r);
+    const ulonglong2 a0 = e[0], a1 = e[1];
+    J[0] = a0.x;
+    J[1] = a0.y;
+    J[2] = a1.x;
+    J[3] = a1.y;
+  }
+  const ulonglong2 st = *reinterpret_cast<const ulonglong2*>(&mp->st_hi);
+  const ulonglong2 inc = *reinterpret_cast<const ulonglong2*>(&mp->inc_hi);
+  const uint4 m4 = *reinterpret_cast<const uint4*>(&mp->has32);
+  const uint32_t* ap = reinterpret_cast<const uint32_t*>(p.actions);
+  const int64_t aw = p.actions_i32 ? env : 2 * env;
+  const uint32_t a_lo = ap[aw], a_hi = ap[p.actions_i32 ? aw : aw + 1];
+  if (!wave_live) return;
+  Pcg rng;
+  rng.hi = st.x;
+  rng.lo = st.y;
+  rng.ihi = inc.x;
+  rng.ilo = inc.y;
+  rng.has32 = m4.x;
+  rng.uinteger = m4.y;
+  int32_t step_count = (int32_t)m4.z;
+  bool fc = (m4.w & 1u) != 0;
+  const int64_t a = p.actions_i32 ? (int64_t)(int32_t)a_lo : (int64_t)(((uint64_t)a_hi << 32) | a_lo);
+  int64_t cell64 = a % A;  // Python modulo (env.py:106)
+  if (cell64 < 0) cell64 += A;
+  const int cell = (int)cell64;
+  const int ar = cell / W_, ac = cell - (cell / W_) * W_;
+  PKSTAMP(1);
+
+  // ---- one reveal (env.py:103-137), per board ----
+  bool done = false;
+  int outcome = MS_OUTCOME_NONE;
+  uint32_t newly = 0;
+  bool mines_changed = false;
+  const bool cell_rev = board_any(r == ar && ((rev >> ac) & 1u), lane);
+  if (!cell_rev) {
+    if (!fc) {
+      const Block B = make_block<H_, W_>(cell, ar, ac, p.K, p.guarantee != 0);
+      bool ok = false;
+      if (!(p.dbg_flags & MS_DBG_FORCE_SERIAL_PLACEMENT)) ok = place_packed<H_, W_>(rng, mine, B, p.K, J, sRow, lane);
+      if (!ok) place_serial_packed(rng, mine, B, p.K, g, lane);
+      fc = true;
+      mines_changed = true;
+    }
+    PKSTAMP(2);
+    const bool hit = board_any(r == ar && ((mine >> ac) & 1u), lane);
+    if (hit) {
+      if (r == ar) rev |= 1u << ac;
+      done = true;
+      outcome = MS_OUTCOME_LOSS;
+    } else {  // flood_fill_reveal (env_numba.py:17-77): dilation to a fixpoint inside the board's row
+      const uint32_t U = row_shr1(mine) | row_shl1(mine);
+      const uint32_t nb = U | (U << 1) | (U >> 1) | (mine << 1) | (mine >> 1);
+      const uint32_t zero = ~nb & ROWMASK;
+      const uint32_t allow = ~mine & ~rev & (r < H_ ? ROWMASK : 0u);
+      uint32_t Fr = (r == ar) ? (1u << ac) : 0u;
+      while (true) {
+        const uint32_t S = Fr & zero;
+        const uint32_t Dh = S | (S << 1) | (S >> 1);
+        const uint32_t Dv = Dh | row_shr1(Dh) | row_shl1(Dh);
+        const uint32_t Fn = Fr | (Dv & allow);
+        const bool changed = __ballot(Fn != Fr) != 0ull;
+        Fr = Fn;
+        if (!changed) break;
+      }
+      rev |= Fr;
+      newly = (uint32_t)__popc(Fr);
+    }
+  }
+  const uint32_t packed = board_sum(((uint32_t)__popc(rev) << 16) | newly);
+  const uint32_t total_rev = packed >> 16;
+  newly = packed & 0xffffu;
+  if (!cell_rev && outcome != MS_OUTCOME_LOSS && (int)total_rev >= A - p.K) {
+    done = true;
+    outcome = MS_OUTCOME_WIN;
+  }
+  PKSTAMP(3);
+  double reward = 0.0;
+  if (outcome == MS_OUTCOME_LOSS) reward += p.loss_reward;
+  if (outcome == MS_OUTCOME_WIN) reward += p.win_reward;
+  reward -= p.step_penalty;
+  step_count += 1;
+  store_aux(p, env, live ? r : kWave, reward, done, step_count, newly, total_rev, outcome, A);
+  if (done) {  // auto-reset (env.py:497-498 -> reset env.py:87-101); RNG continues
+    mine = 0u;
+    rev = 0u;
+    fc = false;
+    step_count = 0;
+    mines_changed = true;
+  }
+  PKSTAMP(4);
+
+  // ---- observation + action mask (env.py:172-196) of the wave's 4 boards: lane 16b+r writes
+  // row r of board b into the LDS image (one ds_write_b32 per cell and channel, offsets
+  // immediate), then the wave copies the image out as whole 1 KiB float4 stores ----
+  if (p.obs || p.mask) {
+    const uint32_t m1 = mine << 1;
+    const uint32_t up1 = row_shr1(m1), dn1 = row_shl1(m1);  // rows r-1, r+1 (0 past the edge)
+    if (r < H_) {
+      float* img = sImg + (lane >> 4) * (10 * A) + r * W_;
+      uint8_t* mk = sMask + (lane >> 4) * A + r * W_;
+#pragma unroll
+      for (int c = 0; c < W_; ++c) {
+        const uint32_t cnt = (uint32_t)__popc((up1 >> c) & 7u) + (uint32_t)__popc((dn1 >> c) & 7u) +
+                             ((m1 >> c) & 1u) + ((m1 >> (c + 2)) & 1u);
+        const uint32_t code = ((rev >> c) & 1u) ? (fc ? 1u + cnt : 10u) : 0u;
+        img[c] = code ? 1.f : 0.f;
+#pragma unroll
+        for (uint32_t ch = 1; ch < 10; ++ch) img[ch * A + c] = code == ch ? 1.f : 0.f;
+        mk[c] = code ? 0 : 1;
+      }
+    }
+    wave_sync();
+    const int nbl = (p.n - env0 < kPackBoards) ? (int)(p.n - env0) : kPackBoards;  // live boards of this wave
+    if (p.obs) {
+      float* ob = p.obs + env0 * 10 * A;
+      if (nbl == kPackBoards) {
+        constexpr int NQ = kPackBoards * 10 * A / 4;
+        const float4* s4 = sImg_all[wv];
+        float4* o4 = reinterpret_cast<float4*>(ob);
+#pragma unroll
+        for (int k = 0; k < NQ / kWave; ++k) o4[k * kWave + lane] = s4[k * kWave + lane];
+        if (NQ % kWave && lane < NQ % kWave) o4[(NQ / kWave) * kWave + lane] = s4[(NQ / kWave) * kWave + lane];
+      } else {  // partial last wave: whole float4s, then the odd tail floats
+        const int nf = nbl * 10 * A;
+        for (int q = lane; q < (nf >> 2); q += kWave) reinterpret_cast<float4*>(ob)[q] = sImg_all[wv][q];
+        for (int f = (nf & ~3) + lane; f < nf; f += kWave) ob[f] = sImg[f];
+      }
+    }
+    if (p.mask) {
+      uint8_t* mb = p.mask + env0 * A;
+      const int nbytes = nbl * A;
+      for (int q = lane; q < (nbytes >> 2); q += kWave) reinterpret_cast<uint32_t*>(mb)[q] = sMask_all[wv][q];
+      for (int i = (nbytes & ~3) + lane; i < nbytes; i += kWave) mb[i] = sMask[i];
+    }
+  }
+  // ---- persist state: meta, then rows -> packed words through this wave's LDS ----
+  store_meta(mp, rng, step_count, fc, live ? r : 1);
+  const int rb = lane & 48;
+  sRow[lane] = mine;
+  wave_sync();
+  if (live && mines_changed && r < NW) {
+    uint64_t acc = 0ull;
+#pragma unroll
+    for (int k = 0; k < RPW; ++k)
+      if (r * RPW + k < H_) acc |= (uint64_t)sRow[rb + r * RPW + k] << (k * W_);
+    mwords[r] = acc;
+  }
+  wave_sync();
+  sRow[lane] = rev;
+  wave_sync();
+  if (live && r < NW) {
+    uint64_t acc = 0ull;
+#pragma unroll
+    for (int k = 0; k < RPW; ++k)
+      if (r * RPW + k < H_) acc |= (uint64_t)sRow[rb + r * RPW + k] << (k * W_);
+    rwords[r] = acc;
+  }
+  PKSTAMP(5);
+}
+
+// ---------------------------------------------------------------------------
 // ms_reset: clear boards (RNG continues) + obs zeros + mask ones.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_reset(EnvMeta* meta, uint64_t* mw, uint64_t* rw, int64_t n,
@@ -1658,6 +2058,17 @@ bool shape_ok(const ms_cfg* c) {
 // difference is the kernel's execution time as the profiler sees it (no launch gap)
 template <int H_, int W_>
 void launch_step(const KParams& p, int epw, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+  if constexpr (packable<H_, W_>()) {
+    // small boards: four per wave (k_step_packed); its float4 / dword stores need a
+    // 16-B obs and 4-B mask base
+    if (p.K >= 1 && p.K <= 16 && !(p.dbg_flags & (MS_DBG_ONE_BOARD_PER_WAVE | MS_DBG_FORCE_CHAIN_PLACEMENT)) &&
+        ((uintptr_t)p.obs & 15u) == 0 && ((uintptr_t)p.mask & 3u) == 0) {
+      constexpr int WPG = 4;
+      const unsigned grid = (unsigned)((p.n + kPackBoards * WPG - 1) / (kPackBoards * WPG));
+      hipExtLaunchKernelGGL((k_step_packed<H_, W_, WPG>), dim3(grid), dim3(64 * WPG), 0, s, ev0, ev1, 0, p);
+      return;
+    }
+  }
   // generic shapes keep one board per workgroup (their LDS table is sized for 64x62)
   if (H_ && W_ && epw == 4) {
     hipExtLaunchKernelGGL((k_step<H_, W_, 4>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, ev0, ev1, 0, p);

@@ -273,6 +273,56 @@ def test_fixpoint_chain_and_serial_placement_agree(gpu, H, W, K):
             assert np.array_equal(v.rng_state(), st), t
 
 
+@pytest.mark.parametrize("H,W,K,N", [(9, 9, 10, 203), (8, 8, 10, 130), (9, 9, 16, 64), (9, 9, 1, 33),
+                                     (9, 9, 10, 1), (9, 9, 10, 6)])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_packed_step_equals_one_board_per_wave(gpu, H, W, K, N, mode):
+    """k_step_packed (four boards per wave in 16-lane DPP rows, per-board RNG in VGPRs,
+    register Floyd chain) is bit-exact with k_step (one board per wave): every output, the
+    mines and the RNG state, at env counts that leave a partial last wave; K = 16 and K = 1
+    are the packed placement's edges. Its forced serial fallback agrees as well."""
+    from ms_amd import _lib as L
+    a, b, c = (_vec(H, W, K, N, seed=17) for _ in range(3))
+    b.set_debug_flags(L.MS_DBG_ONE_BOARD_PER_WAVE)
+    c.set_debug_flags(L.MS_DBG_FORCE_SERIAL_PLACEMENT)
+    for v in (a, b, c):
+        v.reset()
+    for t in range(80):
+        act = a.tape_actions(t, mode)
+        outs = [v.step(act) for v in (a, b, c)]
+        for o in outs[1:]:
+            assert torch.equal(outs[0][0]["obs"], o[0]["obs"]), t
+            assert torch.equal(outs[0][0]["action_mask"], o[0]["action_mask"]), t
+            assert torch.equal(outs[0][1], o[1]) and torch.equal(outs[0][2], o[2]), t
+            for k, x in outs[0][3].tensors.items():
+                assert torch.equal(x, o[3].tensors[k]), (t, k)
+        st = a.rng_state()
+        assert np.array_equal(st, b.rng_state()) and np.array_equal(st, c.rng_state()), t
+    sa, sb = a.snapshot_tensors(), b.snapshot_tensors()
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
+
+
+def test_packed_step_misaligned_obs_falls_back(gpu):
+    """An obs base that is not 16-B aligned (a view one float in) takes k_step; results equal."""
+    from ms_amd import _lib as L
+    a, b = _vec(9, 9, 10, 40, seed=3), _vec(9, 9, 10, 40, seed=3)
+    b.set_debug_flags(L.MS_DBG_ONE_BOARD_PER_WAVE)
+    a.reset()
+    b.reset()
+    for t in range(10):
+        act = a.tape_actions(t, 1)
+        big = torch.empty(40 * 810 + 1, device="cuda")
+        obs = big[1:].view(40, 10, 9, 9)
+        out = dict(obs=obs, action_mask=torch.empty(40, 81, dtype=torch.bool, device="cuda"),
+                   rewards=torch.empty(40, device="cuda"), dones=torch.empty(40, dtype=torch.bool, device="cuda"))
+        a.step(act, out=out)
+        mask = out["action_mask"]
+        ba, ra, da, _ = b.step(act)
+        assert torch.equal(out["rewards"], ra) and torch.equal(out["dones"], da), t
+        assert torch.equal(obs, ba["obs"]) and torch.equal(mask, ba["action_mask"]), t
+
+
 _RUN_KEYS = ("actions", "obs", "action_mask", "rewards", "dones", "step", "last_new_reveals", "revealed_frac",
              "outcome")
 

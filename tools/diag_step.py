@@ -20,12 +20,15 @@ ap.add_argument("--envs", type=int, default=4096)
 ap.add_argument("--board", default="16x16x40")
 ap.add_argument("--tape", type=int, default=0)
 ap.add_argument("--steps", type=int, default=20)
+ap.add_argument("--debug-flags", type=int, default=0, help="MS_DBG_* (4: k_step instead of k_step_packed)")
 args = ap.parse_args()
 H, W, K = (int(x) for x in args.board.split("x"))
 from ms_amd import EnvConfig, VecMinesweeper, _lib as L  # noqa: E402
 
 v = VecMinesweeper(args.envs, EnvConfig(H=H, W=W, mine_count=K), seed=0)
 stamps = torch.zeros((args.envs, 16), dtype=torch.int64, device="cuda")
+if args.debug_flags:
+    v.set_debug_flags(args.debug_flags)
 v.reset()
 for t in range(30):
     v.step(v.tape_actions(t, args.tape))
@@ -41,7 +44,7 @@ for t in range(30, 30 + args.steps):
 S = np.concatenate(rows)
 ph = np.diff(S[:, :6], axis=1).astype(np.float64)
 names = ["loads", "placement", "flood", "reduce+store", "obs"]
-print(f"board {args.board} envs {args.envs} tape {args.tape}: cycles per phase (s_memtime ticks)")
+print(f"board {args.board} envs {args.envs} tape {args.tape} flags {args.debug_flags}: cycles per phase (s_memtime ticks)")
 for i, n in enumerate(names):
     col = ph[:, i]
     print(f"  {n:14s} mean {col.mean():9.0f}  p50 {np.median(col):9.0f}  p99 {np.percentile(col, 99):9.0f}  max {col.max():9.0f}")

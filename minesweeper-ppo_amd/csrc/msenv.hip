@@ -893,26 +893,40 @@ __global__ __launch_bounds__(64 * EPW) void k_step(KParams p) {
 // table in this wave's LDS (wave-local: no workgroup barrier). A 9x9 board fills 9 of
 // 64 lanes in k_step; here 36 of 64, with a quarter of the waves.
 // ---------------------------------------------------------------------------
-constexpr int kPackBoards = 4;  // boards per wave
+
+template <int B>
+__device__ __forceinline__ float ub2f(uint32_t w) {  // byte B of w as f32 (one v_cvt_f32_ubyteB)
+  return (float)((w >> (8 * B)) & 0xffu);
+}
 
 __device__ __forceinline__ uint32_t row_shr1(uint32_t v) { return dpp32<0x111>(v); }  // r <- r-1; r=0 <- 0
 __device__ __forceinline__ uint32_t row_shl1(uint32_t v) { return dpp32<0x101>(v); }  // r <- r+1; r=15 <- 0
-// sum over the board's 16 lanes, result in each of them (row_ror:8,4,2,1)
-__device__ __forceinline__ uint32_t board_sum(uint32_t v) {
+// LPB = lanes per board (16: four boards per wave, 32: two). A board's rows live in the first
+// 16 lanes of its group, so the DPP row ops stay inside one DPP row either way.
+template <int LPB>
+__device__ __forceinline__ int board_base(int lane) { return lane & (64 - LPB); }
+// sum over the board's lanes, result in each of them (row_ror:8,4,2,1; + the other row for 32)
+template <int LPB>
+__device__ __forceinline__ uint32_t board_sum(uint32_t v, int lane) {
   v += dpp32<0x128>(v);
   v += dpp32<0x124>(v);
   v += dpp32<0x122>(v);
   v += dpp32<0x121>(v);
+  if (LPB == 32) v += bperm(v, lane ^ 16);
   return v;
 }
+template <int LPB>
 __device__ __forceinline__ bool board_any(bool v, int lane) {
-  return ((__ballot(v) >> (lane & 48)) & 0xffffull) != 0ull;
+  constexpr uint64_t M = LPB == 64 ? ~0ull : ((1ull << LPB) - 1ull);
+  return ((__ballot(v) >> board_base<LPB>(lane)) & M) != 0ull;
 }
-__device__ __forceinline__ uint32_t board_read(uint32_t v, int lane, int r) {  // v of lane 16b + r
-  return bperm(v, (lane & 48) | (r & 15));
+template <int LPB>
+__device__ __forceinline__ uint32_t board_read(uint32_t v, int lane, int r) {  // v of the board's lane r
+  return bperm(v, board_base<LPB>(lane) | (r & 15));
 }
+template <int LPB>
 __device__ __forceinline__ uint64_t board_read64(uint64_t v, int lane, int r) {
-  return ((uint64_t)board_read((uint32_t)(v >> 32), lane, r) << 32) | board_read((uint32_t)v, lane, r);
+  return ((uint64_t)board_read<LPB>((uint32_t)(v >> 32), lane, r) << 32) | board_read<LPB>((uint32_t)v, lane, r);
 }
 
 // row r (bits r*W .. r*W+W-1) of a 128-bit cell set
@@ -979,10 +993,20 @@ __device__ __forceinline__ int map_block(int t, const Block& B) {
 // and resolves the second by following k (a bpermute per link; chains are short).
 // Mine rows are built with LDS ORs. Returns false on a Lemire rejection, leaving rng
 // untouched (the caller then runs place_serial_packed).
-template <int H_, int W_>
+template <int H_, int W_, int LPB>
 __device__ bool place_packed(Pcg& rng, uint32_t& mine_out, const Block& B, int K, const uint64_t (&J)[4],
-                             uint32_t* sBuf, int lane) {
-  const int r = lane & 15;
+                             uint32_t* sBuf, int lane, uint64_t* dg = nullptr) {
+  const int r = lane & (LPB - 1);
+  (void)dg;
+#ifdef MS_DIAG
+#define QSTAMP(k)                                          \
+  do {                                                     \
+    if (dg && r == 0) dg[(k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define QSTAMP(k) do { } while (0)
+#endif
+  QSTAMP(15);
   const int pop = B.pop;
   const int z0 = (pop == K) ? 1 : 0;
   const int nF = K - z0;
@@ -1007,51 +1031,55 @@ __device__ bool place_packed(Pcg& rng, uint32_t& mine_out, const Block& B, int K
       rej |= lemire_rejects((uint32_t)((uint64_t)d * (bound + 1u)), bound);
     }
   }
-  if (board_any(rej, lane)) return false;
+  if (board_any<LPB>(rej, lane)) return false;
+  QSTAMP(10);
   // lane r: Floyd iteration i = r (draw pidx = i - z0, from output (pidx - h0) / 2)
   const int jr = pop - K + r;
   const int pidx = r - z0;
   const int idx = pidx - h0;
-  const uint32_t wl = board_read((uint32_t)o.x, lane, (idx >> 1) & 15);
-  const uint32_t wh = board_read((uint32_t)(o.x >> 32), lane, (idx >> 1) & 15);
+  const uint32_t wl = board_read<LPB>((uint32_t)o.x, lane, (idx >> 1) & 15);
+  const uint32_t wh = board_read<LPB>((uint32_t)(o.x >> 32), lane, (idx >> 1) & 15);
   uint32_t d = (idx & 1) ? wh : wl;
   if (h0 && pidx == 0) d = rng.uinteger;
   const uint32_t t = r >= K ? 0xffffffffu : (r >= z0 ? (uint32_t)(((uint64_t)d * (uint32_t)(jr + 1)) >> 32) : 0u);
   sBuf[lane] = t;
   wave_sync();
-  const uint4* tb = reinterpret_cast<const uint4*>(sBuf + (lane & 48));
+  const uint4* tb = reinterpret_cast<const uint4*>(sBuf + board_base<LPB>(lane));
   const uint4 q0 = tb[0], q1 = tb[1], q2 = tb[2], q3 = tb[3];
   const uint32_t tk[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
                            q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
   bool dup = false;
 #pragma unroll
   for (int k = 0; k < 15; ++k) dup |= (k < r) && tk[k] == t;
+  QSTAMP(11);
   const int ks = (int)t - (pop - K);  // t == j_ks
   const bool kv = r < K && ks >= 0 && ks < r;
   bool col = dup;
   while (true) {
     // every lane of the board takes part: ds_bpermute returns 0 from an EXEC-disabled source
-    const uint32_t col_ks = board_read(col ? 1u : 0u, lane, ks);
+    const uint32_t col_ks = board_read<LPB>(col ? 1u : 0u, lane, ks);
     const bool nc = dup || (kv && col_ks != 0u);
     const bool changed = __ballot(nc != col) != 0ull;
     col = nc;
     if (!changed) break;
   }
+  QSTAMP(12);
   const int cell = map_block<W_>(col ? jr : (int)t, B);
   wave_sync();
   sBuf[lane] = 0u;
   wave_sync();
-  if (r < K) atomicOr(&sBuf[(lane & 48) + cell / W_], 1u << (cell % W_));
+  if (r < K) atomicOr(&sBuf[board_base<LPB>(lane) + cell / W_], 1u << (cell % W_));
   wave_sync();
   mine_out = r < H_ ? sBuf[lane] : 0u;
   wave_sync();
   if (n_out > 0) {
     const int lq = n_out - 1;
-    rng.hi = board_read64(o.sh, lane, lq);
-    rng.lo = board_read64(o.sl, lane, lq);
-    rng.uinteger = board_read((uint32_t)(o.x >> 32), lane, lq);
+    rng.hi = board_read64<LPB>(o.sh, lane, lq);
+    rng.lo = board_read64<LPB>(o.sl, lane, lq);
+    rng.uinteger = board_read<LPB>((uint32_t)(o.x >> 32), lane, lq);
   }
   if (D > 0) rng.has32 = (uint32_t)(rem & 1);
+  QSTAMP(13);
   return true;
 }
 
@@ -1059,7 +1087,7 @@ __device__ bool place_packed(Pcg& rng, uint32_t& mine_out, const Block& B, int K
 // the same draws on its copy of the board's state (the Lemire-rejection fallback).
 template <int H_, int W_>
 __device__ void place_serial_packed(Pcg& rng, uint32_t& mine_out, const Block& B, int K, const Geo<H_, W_>& g,
-                                    int lane) {
+                                    int r) {
   uint64_t s0 = 0ull, s1 = 0ull;
   for (int j = B.pop - K; j < B.pop; ++j) {
     uint32_t c = (uint32_t)map_block<W_>((int)pcg_bounded(rng, (uint32_t)j), B);
@@ -1067,7 +1095,7 @@ __device__ void place_serial_packed(Pcg& rng, uint32_t& mine_out, const Block& B
     set_add(s0, s1, c);
   }
   for (int i = K - 1; i >= 1; --i) (void)pcg_bounded(rng, (uint32_t)i);  // shuffle draws
-  mine_out = set_row(s0, s1, lane & 15, g);
+  mine_out = set_row(s0, s1, r, g);
 }
 
 template <int H_, int W_>
@@ -1088,27 +1116,32 @@ constexpr bool packable() {
 #define PKSTAMP(k) do { } while (0)
 #endif
 
-template <int H_, int W_, int WPG>
+template <int H_, int W_, int WPG, int BPW>
 __global__ __launch_bounds__(64 * WPG) void k_step_packed(KParams p) {
+  constexpr int LPB = kWave / BPW;  // lanes per board (the board's rows: its first H)
+  static_assert(BPW == 2 || BPW == 4, "boards per wave");
   static_assert(packable<H_, W_>(), "packed board shape");
   constexpr int A = H_ * W_;
   constexpr int RPW = 64 / W_;
   constexpr int NW = (H_ + RPW - 1) / RPW;
   constexpr uint32_t ROWMASK = (1u << W_) - 1u;
-  __shared__ float4 sImg_all[WPG][kPackBoards * 10 * A / 4];  // the 4 boards' obs, as stored
-  __shared__ uint32_t sMask_all[WPG][(kPackBoards * A + 3) / 4];  // their action-mask bytes
+  constexpr int IMG16 = (BPW * 10 * A + 15) / 16;  // 16-B units of the obs byte image
+  __shared__ uint4 sImg_all[WPG][IMG16];  // the 4 boards' obs as 0/1 bytes, in store order
+  __shared__ uint32_t sMask_all[WPG][(BPW * A + 3) / 4];  // their action-mask bytes
   __shared__ __attribute__((aligned(16))) uint32_t sRow_all[WPG][kWave];
+  __shared__ uint32_t sRev_all[WPG][kWave];
   const int lane = lane_id();
-  const int r = lane & 15;
+  const int r = lane & (LPB - 1);
   const int wv = (WPG == 1) ? 0 : (int)rfl(threadIdx.x >> 6);
-  const int64_t env0 = ((int64_t)blockIdx.x * WPG + wv) * kPackBoards;
+  const int64_t env0 = ((int64_t)blockIdx.x * WPG + wv) * BPW;
   const bool wave_live = env0 < p.n;
-  const int64_t env_raw = env0 + (lane >> 4);
+  const int64_t env_raw = env0 + (lane / LPB);
   const bool live = env_raw < p.n;
   const int64_t env = live ? env_raw : p.n - 1;  // a board past the end loads env n-1, stores nothing
-  float* sImg = reinterpret_cast<float*>(sImg_all[wv]);
+  uint8_t* sImg = reinterpret_cast<uint8_t*>(sImg_all[wv]);
   uint8_t* sMask = reinterpret_cast<uint8_t*>(sMask_all[wv]);
   uint32_t* sRow = sRow_all[wv];
+  uint32_t* sRev = sRev_all[wv];
   const Geo<H_, W_> g(H_, W_);
   PKSTAMP(0);
 
@@ -1154,18 +1187,19 @@ __global__ __launch_bounds__(64 * WPG) void k_step_packed(KParams p) {
   int outcome = MS_OUTCOME_NONE;
   uint32_t newly = 0;
   bool mines_changed = false;
-  const bool cell_rev = board_any(r == ar && ((rev >> ac) & 1u), lane);
+  const bool cell_rev = board_any<LPB>(r == ar && ((rev >> ac) & 1u), lane);
   if (!cell_rev) {
     if (!fc) {
       const Block B = make_block<H_, W_>(cell, ar, ac, p.K, p.guarantee != 0);
       bool ok = false;
-      if (!(p.dbg_flags & MS_DBG_FORCE_SERIAL_PLACEMENT)) ok = place_packed<H_, W_>(rng, mine, B, p.K, J, sRow, lane);
-      if (!ok) place_serial_packed(rng, mine, B, p.K, g, lane);
+      if (!(p.dbg_flags & MS_DBG_FORCE_SERIAL_PLACEMENT))
+        ok = place_packed<H_, W_, LPB>(rng, mine, B, p.K, J, sRow, lane, (p.diag && live) ? p.diag + env * 16 : nullptr);
+      if (!ok) place_serial_packed(rng, mine, B, p.K, g, r);
       fc = true;
       mines_changed = true;
     }
     PKSTAMP(2);
-    const bool hit = board_any(r == ar && ((mine >> ac) & 1u), lane);
+    const bool hit = board_any<LPB>(r == ar && ((mine >> ac) & 1u), lane);
     if (hit) {
       if (r == ar) rev |= 1u << ac;
       done = true;
@@ -1189,7 +1223,7 @@ __global__ __launch_bounds__(64 * WPG) void k_step_packed(KParams p) {
       newly = (uint32_t)__popc(Fr);
     }
   }
-  const uint32_t packed = board_sum(((uint32_t)__popc(rev) << 16) | newly);
+  const uint32_t packed = board_sum<LPB>(((uint32_t)__popc(rev) << 16) | newly, lane);
   const uint32_t total_rev = packed >> 16;
   newly = packed & 0xffffu;
   if (!cell_rev && outcome != MS_OUTCOME_LOSS && (int)total_rev >= A - p.K) {
@@ -1212,71 +1246,92 @@ __global__ __launch_bounds__(64 * WPG) void k_step_packed(KParams p) {
   }
   PKSTAMP(4);
 
-  // ---- observation + action mask (env.py:172-196) of the wave's 4 boards: lane 16b+r writes
-  // row r of board b into the LDS image (one ds_write_b32 per cell and channel, offsets
-  // immediate), then the wave copies the image out as whole 1 KiB float4 stores ----
+  // ---- observation + action mask (env.py:172-196) of the wave's 4 boards. The obs are
+  // one-hot, so the wave zero-fills a byte image of them in LDS, each lane 16b+r sets the
+  // (at most two) 1 bytes of each revealed cell of row r, and the wave copies the image out
+  // as whole 1 KiB float4 stores (4 bytes -> 4 floats: v_cvt_f32_ubyte0..3) ----
   if (p.obs || p.mask) {
+#pragma unroll
+    for (int k = 0; k < (IMG16 + kWave - 1) / kWave; ++k)
+      if (k * kWave + lane < IMG16) sImg_all[wv][k * kWave + lane] = make_uint4(0u, 0u, 0u, 0u);
     const uint32_t m1 = mine << 1;
     const uint32_t up1 = row_shr1(m1), dn1 = row_shl1(m1);  // rows r-1, r+1 (0 past the edge)
+    wave_sync();
     if (r < H_) {
-      float* img = sImg + (lane >> 4) * (10 * A) + r * W_;
-      uint8_t* mk = sMask + (lane >> 4) * A + r * W_;
+      uint8_t* img = sImg + (lane / LPB) * (10 * A) + r * W_;
+      uint8_t* mk = sMask + (lane / LPB) * A + r * W_;
 #pragma unroll
       for (int c = 0; c < W_; ++c) {
         const uint32_t cnt = (uint32_t)__popc((up1 >> c) & 7u) + (uint32_t)__popc((dn1 >> c) & 7u) +
                              ((m1 >> c) & 1u) + ((m1 >> (c + 2)) & 1u);
-        const uint32_t code = ((rev >> c) & 1u) ? (fc ? 1u + cnt : 10u) : 0u;
-        img[c] = code ? 1.f : 0.f;
-#pragma unroll
-        for (uint32_t ch = 1; ch < 10; ++ch) img[ch * A + c] = code == ch ? 1.f : 0.f;
-        mk[c] = code ? 0 : 1;
+        const uint32_t rv = (rev >> c) & 1u;
+        mk[c] = (uint8_t)(rv ^ 1u);
+        // unconditional byte stores, no branch per cell: channel 0 = revealed, channel 1 + count
+        // = 1 for a revealed cell after the first click (env.py:183-190); a hidden cell writes a
+        // 0 over the zero-filled byte of its channel 1 + count
+        img[c] = (uint8_t)rv;
+        img[(1 + cnt) * A + c] = (uint8_t)(fc ? rv : 0u);
       }
     }
+    PKSTAMP(8);
     wave_sync();
-    const int nbl = (p.n - env0 < kPackBoards) ? (int)(p.n - env0) : kPackBoards;  // live boards of this wave
+    const int nbl = (p.n - env0 < BPW) ? (int)(p.n - env0) : BPW;  // live boards of this wave
     if (p.obs) {
       float* ob = p.obs + env0 * 10 * A;
-      if (nbl == kPackBoards) {
-        constexpr int NQ = kPackBoards * 10 * A / 4;
-        const float4* s4 = sImg_all[wv];
+      const uint32_t* s32 = reinterpret_cast<const uint32_t*>(sImg);
+      if (nbl == BPW) {
+        constexpr int NQ = BPW * 10 * A / 4;
         float4* o4 = reinterpret_cast<float4*>(ob);
 #pragma unroll
-        for (int k = 0; k < NQ / kWave; ++k) o4[k * kWave + lane] = s4[k * kWave + lane];
-        if (NQ % kWave && lane < NQ % kWave) o4[(NQ / kWave) * kWave + lane] = s4[(NQ / kWave) * kWave + lane];
+        for (int k = 0; k < (NQ + kWave - 1) / kWave; ++k) {
+          const int q = k * kWave + lane;
+          if (q < NQ) {
+            const uint32_t w = s32[q];
+            o4[q] = make_float4(ub2f<0>(w), ub2f<1>(w),
+                                ub2f<2>(w), ub2f<3>(w));
+          }
+        }
       } else {  // partial last wave: whole float4s, then the odd tail floats
         const int nf = nbl * 10 * A;
-        for (int q = lane; q < (nf >> 2); q += kWave) reinterpret_cast<float4*>(ob)[q] = sImg_all[wv][q];
-        for (int f = (nf & ~3) + lane; f < nf; f += kWave) ob[f] = sImg[f];
+        for (int q = lane; q < (nf >> 2); q += kWave) {
+          const uint32_t w = s32[q];
+          reinterpret_cast<float4*>(ob)[q] =
+              make_float4(ub2f<0>(w), ub2f<1>(w),
+                          ub2f<2>(w), ub2f<3>(w));
+        }
+        for (int f = (nf & ~3) + lane; f < nf; f += kWave) ob[f] = (float)sImg[f];
       }
     }
+    PKSTAMP(9);
     if (p.mask) {
       uint8_t* mb = p.mask + env0 * A;
       const int nbytes = nbl * A;
-      for (int q = lane; q < (nbytes >> 2); q += kWave) reinterpret_cast<uint32_t*>(mb)[q] = sMask_all[wv][q];
-      for (int i = (nbytes & ~3) + lane; i < nbytes; i += kWave) mb[i] = sMask[i];
+      if (BPW == 4) {  // env0 * A is a multiple of 4
+        for (int q = lane; q < (nbytes >> 2); q += kWave) reinterpret_cast<uint32_t*>(mb)[q] = sMask_all[wv][q];
+        for (int i = (nbytes & ~3) + lane; i < nbytes; i += kWave) mb[i] = sMask[i];
+      } else {  // a multiple of 2
+        const uint16_t* m16 = reinterpret_cast<const uint16_t*>(sMask);
+        for (int q = lane; q < (nbytes >> 1); q += kWave) reinterpret_cast<uint16_t*>(mb)[q] = m16[q];
+        if ((nbytes & 1) && lane == 0) mb[nbytes - 1] = sMask[nbytes - 1];
+      }
     }
   }
   // ---- persist state: meta, then rows -> packed words through this wave's LDS ----
   store_meta(mp, rng, step_count, fc, live ? r : 1);
-  const int rb = lane & 48;
+  const int rb = board_base<LPB>(lane);
   sRow[lane] = mine;
-  wave_sync();
-  if (live && mines_changed && r < NW) {
-    uint64_t acc = 0ull;
-#pragma unroll
-    for (int k = 0; k < RPW; ++k)
-      if (r * RPW + k < H_) acc |= (uint64_t)sRow[rb + r * RPW + k] << (k * W_);
-    mwords[r] = acc;
-  }
-  wave_sync();
-  sRow[lane] = rev;
+  sRev[lane] = rev;
   wave_sync();
   if (live && r < NW) {
-    uint64_t acc = 0ull;
+    uint64_t am = 0ull, ar_ = 0ull;
 #pragma unroll
     for (int k = 0; k < RPW; ++k)
-      if (r * RPW + k < H_) acc |= (uint64_t)sRow[rb + r * RPW + k] << (k * W_);
-    rwords[r] = acc;
+      if (r * RPW + k < H_) {
+        am |= (uint64_t)sRow[rb + r * RPW + k] << (k * W_);
+        ar_ |= (uint64_t)sRev[rb + r * RPW + k] << (k * W_);
+      }
+    if (mines_changed) mwords[r] = am;
+    rwords[r] = ar_;
   }
   PKSTAMP(5);
 }
@@ -2064,8 +2119,13 @@ void launch_step(const KParams& p, int epw, hipStream_t s, hipEvent_t ev0, hipEv
     if (p.K >= 1 && p.K <= 16 && !(p.dbg_flags & (MS_DBG_ONE_BOARD_PER_WAVE | MS_DBG_FORCE_CHAIN_PLACEMENT)) &&
         ((uintptr_t)p.obs & 15u) == 0 && ((uintptr_t)p.mask & 3u) == 0) {
       constexpr int WPG = 4;
-      const unsigned grid = (unsigned)((p.n + kPackBoards * WPG - 1) / (kPackBoards * WPG));
-      hipExtLaunchKernelGGL((k_step_packed<H_, W_, WPG>), dim3(grid), dim3(64 * WPG), 0, s, ev0, ev1, 0, p);
+      if (p.dbg_flags & MS_DBG_TWO_BOARDS_PER_WAVE) {
+        const unsigned grid = (unsigned)((p.n + 2 * WPG - 1) / (2 * WPG));
+        hipExtLaunchKernelGGL((k_step_packed<H_, W_, WPG, 2>), dim3(grid), dim3(64 * WPG), 0, s, ev0, ev1, 0, p);
+      } else {
+        const unsigned grid = (unsigned)((p.n + 4 * WPG - 1) / (4 * WPG));
+        hipExtLaunchKernelGGL((k_step_packed<H_, W_, WPG, 4>), dim3(grid), dim3(64 * WPG), 0, s, ev0, ev1, 0, p);
+      }
       return;
     }
   }

@@ -280,16 +280,18 @@ def test_packed_step_equals_one_board_per_wave(gpu, H, W, K, N, mode):
     """k_step_packed (four boards per wave in 16-lane DPP rows, per-board RNG in VGPRs,
     register Floyd chain) is bit-exact with k_step (one board per wave): every output, the
     mines and the RNG state, at env counts that leave a partial last wave; K = 16 and K = 1
-    are the packed placement's edges. Its forced serial fallback agrees as well."""
+    are the packed placement's edges. Its forced serial fallback and the two-boards-per-wave
+    form (32-lane groups) agree as well."""
     from ms_amd import _lib as L
-    a, b, c = (_vec(H, W, K, N, seed=17) for _ in range(3))
+    a, b, c, d = (_vec(H, W, K, N, seed=17) for _ in range(4))
     b.set_debug_flags(L.MS_DBG_ONE_BOARD_PER_WAVE)
     c.set_debug_flags(L.MS_DBG_FORCE_SERIAL_PLACEMENT)
-    for v in (a, b, c):
+    d.set_debug_flags(L.MS_DBG_TWO_BOARDS_PER_WAVE)
+    for v in (a, b, c, d):
         v.reset()
     for t in range(80):
         act = a.tape_actions(t, mode)
-        outs = [v.step(act) for v in (a, b, c)]
+        outs = [v.step(act) for v in (a, b, c, d)]
         for o in outs[1:]:
             assert torch.equal(outs[0][0]["obs"], o[0]["obs"]), t
             assert torch.equal(outs[0][0]["action_mask"], o[0]["action_mask"]), t
@@ -297,7 +299,7 @@ def test_packed_step_equals_one_board_per_wave(gpu, H, W, K, N, mode):
             for k, x in outs[0][3].tensors.items():
                 assert torch.equal(x, o[3].tensors[k]), (t, k)
         st = a.rng_state()
-        assert np.array_equal(st, b.rng_state()) and np.array_equal(st, c.rng_state()), t
+        assert all(np.array_equal(st, v.rng_state()) for v in (b, c, d)), t
     sa, sb = a.snapshot_tensors(), b.snapshot_tensors()
     for k in sa:
         assert torch.equal(sa[k], sb[k]), k

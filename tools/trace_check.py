@@ -5,7 +5,7 @@ can be checked against profiles/.
     python tools/trace_check.py --trace DIR --line bench_line_n1.json --out trace_check.json
 
 k_step: mean dispatch duration of the config's grid (one 64-lane wave per env: grid
-threads = 64 * envs) -> algorithmic bytes / duration. k_run: the config's dispatches
+threads = 64 * envs; k_step_packed, four boards per wave, is keyed the same way) -> algorithmic bytes / duration. k_run: the config's dispatches
 minus the first (the untimed warm-up launch), summed and divided by the timed steps (the
 multistep record's timed_steps: bench.py times max(--steps, --min-timed-steps) of them).
 """
@@ -41,10 +41,14 @@ def grid_threads(r):
 disp = defaultdict(list)  # (kernel tag, board, grid threads) -> [(start, dur_ns)]
 for r in rows:
     name = r["Kernel_Name"]
-    for tag in ("k_step", "k_run"):
-        if f"{tag}<" in name:
-            board = name.split(f"{tag}<", 1)[1].split(">", 1)[0].split(",")[:2]
-            key = (tag, f"{int(board[0])}x{int(board[1])}", grid_threads(r))
+    # k_step_packed (four small boards per wave) is the k_step of 9x9 / 8x8 boards
+    for tag, pat in (("k_step", "k_step<"), ("k_step", "k_step_packed<"), ("k_run", "k_run<")):
+        if pat in name:
+            board = name.split(pat, 1)[1].split(">", 1)[0].split(",")[:2]
+            g = grid_threads(r)
+            if pat == "k_step_packed<":
+                g *= 4  # 16 boards per 256-thread workgroup -> the same key as 64 lanes per board
+            key = (tag, f"{int(board[0])}x{int(board[1])}", g)
             disp[key].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
 
 line = json.loads(open(a.line).read())

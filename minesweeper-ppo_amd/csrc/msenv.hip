@@ -1103,102 +1103,58 @@ constexpr bool packable() {
   return H_ >= 1 && H_ <= 16 && W_ >= 1 && W_ <= 31 && H_ * W_ <= 128;
 }
 
+// MS_DIAG builds: per-board phase stamps into this env's diag row (lane r == 0 of the board)
 #ifdef MS_DIAG
-#define PKSTAMP(k)                                                            \
-  do {                                                                        \
-    if (p.diag && r == 0 && live) {                                           \
-      p.diag[env * 16 + (k)] = __builtin_amdgcn_s_memtime();                  \
-      if ((k) == 0) p.diag[env * 16 + 6] = __builtin_amdgcn_s_memrealtime();  \
-      if ((k) == 5) p.diag[env * 16 + 7] = __builtin_amdgcn_s_memrealtime();  \
-    }                                                                         \
+#define DSTAMP(k)                                                            \
+  do {                                                                       \
+    if (dgs && r == 0) {                                                     \
+      dgs[(k)] = __builtin_amdgcn_s_memtime();                               \
+      if ((k) == 0) dgs[6] = __builtin_amdgcn_s_memrealtime();               \
+      if ((k) == 5) dgs[7] = __builtin_amdgcn_s_memrealtime();               \
+    }                                                                        \
   } while (0)
 #else
-#define PKSTAMP(k) do { } while (0)
+#define DSTAMP(k) do { } while (0)
 #endif
 
-template <int H_, int W_, int WPG, int BPW>
-__global__ __launch_bounds__(64 * WPG) void k_step_packed(KParams p) {
-  constexpr int LPB = kWave / BPW;  // lanes per board (the board's rows: its first H)
-  static_assert(BPW == 2 || BPW == 4, "boards per wave");
-  static_assert(packable<H_, W_>(), "packed board shape");
+// LDS of one wave of the packed kernels
+template <int H_, int W_, int BPW>
+struct PackedLds {
+  static constexpr int A = H_ * W_;
+  static constexpr int IMG16 = (BPW * 10 * A + 15) / 16;  // 16-B units of the obs byte image
+  uint4 img[IMG16];                     // the wave's boards' obs as 0/1 bytes, in store order
+  uint32_t mask[(BPW * A + 3) / 4];     // their action-mask bytes
+  alignas(16) uint32_t row[kWave];      // placement scratch; mine rows for the word store
+  uint32_t rev[kWave];                  // revealed rows for the word store
+};
+
+// One reveal on each board of the wave (env.py:103-137 minus the reward / step bookkeeping):
+// first-click placement, mine hit, flood fill, win check. Per-board results are uniform
+// across the board's lanes.
+template <int H_, int W_, int LPB>
+__device__ __forceinline__ void pk_click(const KParams& p, Pcg& rng, uint32_t& mine, uint32_t& rev, bool& fc, int cell,
+                                         const uint64_t (&J)[4], uint32_t* sRow, int lane, uint64_t* dgs,
+                                         bool& done, int& outcome, uint32_t& newly, uint32_t& total_rev,
+                                         bool& mines_changed, bool& cell_rev) {
   constexpr int A = H_ * W_;
-  constexpr int RPW = 64 / W_;
-  constexpr int NW = (H_ + RPW - 1) / RPW;
   constexpr uint32_t ROWMASK = (1u << W_) - 1u;
-  constexpr int IMG16 = (BPW * 10 * A + 15) / 16;  // 16-B units of the obs byte image
-  __shared__ uint4 sImg_all[WPG][IMG16];  // the 4 boards' obs as 0/1 bytes, in store order
-  __shared__ uint32_t sMask_all[WPG][(BPW * A + 3) / 4];  // their action-mask bytes
-  __shared__ __attribute__((aligned(16))) uint32_t sRow_all[WPG][kWave];
-  __shared__ uint32_t sRev_all[WPG][kWave];
-  const int lane = lane_id();
   const int r = lane & (LPB - 1);
-  const int wv = (WPG == 1) ? 0 : (int)rfl(threadIdx.x >> 6);
-  const int64_t env0 = ((int64_t)blockIdx.x * WPG + wv) * BPW;
-  const bool wave_live = env0 < p.n;
-  const int64_t env_raw = env0 + (lane / LPB);
-  const bool live = env_raw < p.n;
-  const int64_t env = live ? env_raw : p.n - 1;  // a board past the end loads env n-1, stores nothing
-  uint8_t* sImg = reinterpret_cast<uint8_t*>(sImg_all[wv]);
-  uint8_t* sMask = reinterpret_cast<uint8_t*>(sMask_all[wv]);
-  uint32_t* sRow = sRow_all[wv];
-  uint32_t* sRev = sRev_all[wv];
   const Geo<H_, W_> g(H_, W_);
-  PKSTAMP(0);
-
-  EnvMeta* mp = p.meta + env;
-  uint64_t* mwords = p.mine_words + env * NW;
-  uint64_t* rwords = p.rev_words + env * NW;
-  uint32_t mine = (uint32_t)load_row(mwords, g, r);
-  uint32_t rev = (uint32_t)load_row(rwords, g, r);
-  uint64_t J[4] = {0ull, 0ull, 0ull, 0ull};  // jump entry k = r+1 (a placement uses outputs 1..K)
-  if (r < p.K) {
-    const ulonglong2* e = reinterpret_cast<const ulonglong2*>(p.jump + 4 * r);
-    const ulonglong2 a0 = e[0], a1 = e[1];
-    J[0] = a0.x;
-    J[1] = a0.y;
-    J[2] = a1.x;
-    J[3] = a1.y;
-  }
-  const ulonglong2 st = *reinterpret_cast<const ulonglong2*>(&mp->st_hi);
-  const ulonglong2 inc = *reinterpret_cast<const ulonglong2*>(&mp->inc_hi);
-  const uint4 m4 = *reinterpret_cast<const uint4*>(&mp->has32);
-  const uint32_t* ap = reinterpret_cast<const uint32_t*>(p.actions);
-  const int64_t aw = p.actions_i32 ? env : 2 * env;
-  const uint32_t a_lo = ap[aw], a_hi = ap[p.actions_i32 ? aw : aw + 1];
-  if (!wave_live) return;
-  Pcg rng;
-  rng.hi = st.x;
-  rng.lo = st.y;
-  rng.ihi = inc.x;
-  rng.ilo = inc.y;
-  rng.has32 = m4.x;
-  rng.uinteger = m4.y;
-  int32_t step_count = (int32_t)m4.z;
-  bool fc = (m4.w & 1u) != 0;
-  const int64_t a = p.actions_i32 ? (int64_t)(int32_t)a_lo : (int64_t)(((uint64_t)a_hi << 32) | a_lo);
-  int64_t cell64 = a % A;  // Python modulo (env.py:106)
-  if (cell64 < 0) cell64 += A;
-  const int cell = (int)cell64;
   const int ar = cell / W_, ac = cell - (cell / W_) * W_;
-  PKSTAMP(1);
-
-  // ---- one reveal (env.py:103-137), per board ----
-  bool done = false;
-  int outcome = MS_OUTCOME_NONE;
-  uint32_t newly = 0;
-  bool mines_changed = false;
-  const bool cell_rev = board_any<LPB>(r == ar && ((rev >> ac) & 1u), lane);
+  done = false;
+  outcome = MS_OUTCOME_NONE;
+  newly = 0;
+  cell_rev = board_any<LPB>(r == ar && ((rev >> ac) & 1u), lane);
   if (!cell_rev) {
     if (!fc) {
       const Block B = make_block<H_, W_>(cell, ar, ac, p.K, p.guarantee != 0);
       bool ok = false;
-      if (!(p.dbg_flags & MS_DBG_FORCE_SERIAL_PLACEMENT))
-        ok = place_packed<H_, W_, LPB>(rng, mine, B, p.K, J, sRow, lane, (p.diag && live) ? p.diag + env * 16 : nullptr);
+      if (!(p.dbg_flags & MS_DBG_FORCE_SERIAL_PLACEMENT)) ok = place_packed<H_, W_, LPB>(rng, mine, B, p.K, J, sRow, lane, dgs);
       if (!ok) place_serial_packed(rng, mine, B, p.K, g, r);
       fc = true;
       mines_changed = true;
     }
-    PKSTAMP(2);
+    DSTAMP(2);
     const bool hit = board_any<LPB>(r == ar && ((mine >> ac) & 1u), lane);
     if (hit) {
       if (r == ar) rev |= 1u << ac;
@@ -1224,13 +1180,188 @@ __global__ __launch_bounds__(64 * WPG) void k_step_packed(KParams p) {
     }
   }
   const uint32_t packed = board_sum<LPB>(((uint32_t)__popc(rev) << 16) | newly, lane);
-  const uint32_t total_rev = packed >> 16;
+  total_rev = packed >> 16;
   newly = packed & 0xffffu;
   if (!cell_rev && outcome != MS_OUTCOME_LOSS && (int)total_rev >= A - p.K) {
     done = true;
     outcome = MS_OUTCOME_WIN;
   }
-  PKSTAMP(3);
+}
+
+// Observation + action mask (env.py:172-196) of the wave's nbl live boards, written to the
+// contiguous chunks ob (nbl*10*A floats, 16-B aligned) and mb (nbl*A bytes, 4-B aligned for
+// BPW = 4, 2-B for BPW = 2). The obs are one-hot, so the wave zero-fills a byte image of them
+// in LDS, each lane sets the (at most two) 1 bytes of each revealed cell of its row, and the
+// wave copies the image out as whole 1 KiB float4 stores (4 bytes -> 4 floats with
+// v_cvt_f32_ubyte0..3).
+template <int H_, int W_, int BPW, int LPB>
+__device__ __forceinline__ void pk_emit(float* ob, uint8_t* mb, int nbl, uint32_t mine, uint32_t rev, bool fc,
+                                        PackedLds<H_, W_, BPW>& S, int lane, uint64_t* dgs) {
+  constexpr int A = H_ * W_;
+  constexpr int IMG16 = PackedLds<H_, W_, BPW>::IMG16;
+  const int r = lane & (LPB - 1);
+  uint8_t* sImg = reinterpret_cast<uint8_t*>(S.img);
+  uint8_t* sMask = reinterpret_cast<uint8_t*>(S.mask);
+#pragma unroll
+  for (int k = 0; k < (IMG16 + kWave - 1) / kWave; ++k)
+    if (k * kWave + lane < IMG16) S.img[k * kWave + lane] = make_uint4(0u, 0u, 0u, 0u);
+  const uint32_t m1 = mine << 1;
+  const uint32_t up1 = row_shr1(m1), dn1 = row_shl1(m1);  // rows r-1, r+1 (0 past the edge)
+  wave_sync();
+  if (r < H_) {
+    uint8_t* img = sImg + (lane / LPB) * (10 * A) + r * W_;
+    uint8_t* mk = sMask + (lane / LPB) * A + r * W_;
+#pragma unroll
+    for (int c = 0; c < W_; ++c) {
+      const uint32_t cnt = (uint32_t)__popc((up1 >> c) & 7u) + (uint32_t)__popc((dn1 >> c) & 7u) +
+                           ((m1 >> c) & 1u) + ((m1 >> (c + 2)) & 1u);
+      const uint32_t rv = (rev >> c) & 1u;
+      mk[c] = (uint8_t)(rv ^ 1u);
+      // unconditional byte stores, no branch per cell: channel 0 = revealed, channel 1 + count
+      // = 1 for a revealed cell after the first click (env.py:183-190); a hidden cell writes a
+      // 0 over the zero-filled byte of its channel 1 + count
+      img[c] = (uint8_t)rv;
+      img[(1 + cnt) * A + c] = (uint8_t)(fc ? rv : 0u);
+    }
+  }
+  DSTAMP(8);
+  wave_sync();
+  if (ob) {
+    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(sImg);
+    if (nbl == BPW) {
+      constexpr int NQ = BPW * 10 * A / 4;
+      float4* o4 = reinterpret_cast<float4*>(ob);
+#pragma unroll
+      for (int k = 0; k < (NQ + kWave - 1) / kWave; ++k) {
+        const int q = k * kWave + lane;
+        if (q < NQ) {
+          const uint32_t w = s32[q];
+          o4[q] = make_float4(ub2f<0>(w), ub2f<1>(w), ub2f<2>(w), ub2f<3>(w));
+        }
+      }
+    } else {  // partial last wave: whole float4s, then the odd tail floats
+      const int nf = nbl * 10 * A;
+      for (int q = lane; q < (nf >> 2); q += kWave) {
+        const uint32_t w = s32[q];
+        reinterpret_cast<float4*>(ob)[q] = make_float4(ub2f<0>(w), ub2f<1>(w), ub2f<2>(w), ub2f<3>(w));
+      }
+      for (int f = (nf & ~3) + lane; f < nf; f += kWave) ob[f] = (float)sImg[f];
+    }
+  }
+  DSTAMP(9);
+  if (mb) {
+    const int nbytes = nbl * A;
+    if (BPW == 4) {
+      for (int q = lane; q < (nbytes >> 2); q += kWave) reinterpret_cast<uint32_t*>(mb)[q] = S.mask[q];
+      for (int i = (nbytes & ~3) + lane; i < nbytes; i += kWave) mb[i] = sMask[i];
+    } else {
+      const uint16_t* m16 = reinterpret_cast<const uint16_t*>(sMask);
+      for (int q = lane; q < (nbytes >> 1); q += kWave) reinterpret_cast<uint16_t*>(mb)[q] = m16[q];
+      if ((nbytes & 1) && lane == 0) mb[nbytes - 1] = sMask[nbytes - 1];
+    }
+  }
+}
+
+// EnvMeta and the row words of each live board (rows -> packed words through LDS)
+template <int H_, int W_, int BPW, int LPB>
+__device__ __forceinline__ void pk_store_state(EnvMeta* mp, uint64_t* mwords, uint64_t* rwords, const Pcg& rng,
+                                               int32_t step_count, bool fc, uint32_t mine, uint32_t rev,
+                                               bool mines_changed, bool live, PackedLds<H_, W_, BPW>& S, int lane) {
+  constexpr int RPW = 64 / W_;
+  constexpr int NW = (H_ + RPW - 1) / RPW;
+  const int r = lane & (LPB - 1);
+  store_meta(mp, rng, step_count, fc, live ? r : 1);
+  const int rb = board_base<LPB>(lane);
+  S.row[lane] = mine;
+  S.rev[lane] = rev;
+  wave_sync();
+  if (live && r < NW) {
+    uint64_t am = 0ull, ar_ = 0ull;
+#pragma unroll
+    for (int k = 0; k < RPW; ++k)
+      if (r * RPW + k < H_) {
+        am |= (uint64_t)S.row[rb + r * RPW + k] << (k * W_);
+        ar_ |= (uint64_t)S.rev[rb + r * RPW + k] << (k * W_);
+      }
+    if (mines_changed) mwords[r] = am;
+    rwords[r] = ar_;
+  }
+}
+
+// Loads of one packed board: rows, this lane's jump entry (k = r+1: a placement uses outputs
+// 1..K), and the meta (every lane of the board reads the same 48 B)
+template <int H_, int W_>
+__device__ __forceinline__ void pk_load(const KParams& p, int64_t env, int r, uint32_t& mine, uint32_t& rev,
+                                        uint64_t (&J)[4], Pcg& rng, int32_t& step_count, bool& fc) {
+  constexpr int RPW = 64 / W_;
+  constexpr int NW = (H_ + RPW - 1) / RPW;
+  const Geo<H_, W_> g(H_, W_);
+  const EnvMeta* mp = p.meta + env;
+  mine = (uint32_t)load_row(p.mine_words + env * NW, g, r);
+  rev = (uint32_t)load_row(p.rev_words + env * NW, g, r);
+  J[0] = J[1] = J[2] = J[3] = 0ull;
+  if (r < p.K) {
+    const ulonglong2* e = reinterpret_cast<const ulonglong2*>(p.jump + 4 * r);
+    const ulonglong2 a0 = e[0], a1 = e[1];
+    J[0] = a0.x;
+    J[1] = a0.y;
+    J[2] = a1.x;
+    J[3] = a1.y;
+  }
+  const ulonglong2 st = *reinterpret_cast<const ulonglong2*>(&mp->st_hi);
+  const ulonglong2 inc = *reinterpret_cast<const ulonglong2*>(&mp->inc_hi);
+  const uint4 m4 = *reinterpret_cast<const uint4*>(&mp->has32);
+  rng.hi = st.x;
+  rng.lo = st.y;
+  rng.ihi = inc.x;
+  rng.ilo = inc.y;
+  rng.has32 = m4.x;
+  rng.uinteger = m4.y;
+  step_count = (int32_t)m4.z;
+  fc = (m4.w & 1u) != 0;
+}
+
+template <int H_, int W_, int WPG, int BPW>
+__global__ __launch_bounds__(64 * WPG) void k_step_packed(KParams p) {
+  constexpr int LPB = kWave / BPW;  // lanes per board (the board's rows: its first H)
+  static_assert(BPW == 2 || BPW == 4, "boards per wave");
+  static_assert(packable<H_, W_>(), "packed board shape");
+  constexpr int A = H_ * W_;
+  constexpr int RPW = 64 / W_;
+  constexpr int NW = (H_ + RPW - 1) / RPW;
+  __shared__ PackedLds<H_, W_, BPW> S_all[WPG];
+  const int lane = lane_id();
+  const int r = lane & (LPB - 1);
+  const int wv = (WPG == 1) ? 0 : (int)rfl(threadIdx.x >> 6);
+  PackedLds<H_, W_, BPW>& S = S_all[wv];
+  const int64_t env0 = ((int64_t)blockIdx.x * WPG + wv) * BPW;
+  const bool wave_live = env0 < p.n;
+  const int64_t env_raw = env0 + (lane / LPB);
+  const bool live = env_raw < p.n;
+  const int64_t env = live ? env_raw : p.n - 1;  // a board past the end loads env n-1, stores nothing
+  uint64_t* dgs = (p.diag && live) ? p.diag + env * 16 : nullptr;
+  (void)dgs;
+  DSTAMP(0);
+  uint32_t mine, rev;
+  uint64_t J[4];
+  Pcg rng;
+  int32_t step_count;
+  bool fc;
+  pk_load<H_, W_>(p, env, r, mine, rev, J, rng, step_count, fc);
+  const uint32_t* ap = reinterpret_cast<const uint32_t*>(p.actions);
+  const int64_t aw = p.actions_i32 ? env : 2 * env;
+  const uint32_t a_lo = ap[aw], a_hi = ap[p.actions_i32 ? aw : aw + 1];
+  if (!wave_live) return;
+  const int64_t a = p.actions_i32 ? (int64_t)(int32_t)a_lo : (int64_t)(((uint64_t)a_hi << 32) | a_lo);
+  int64_t cell64 = a % A;  // Python modulo (env.py:106)
+  if (cell64 < 0) cell64 += A;
+  DSTAMP(1);
+  bool done, mines_changed = false, cell_rev;
+  int outcome;
+  uint32_t newly, total_rev;
+  pk_click<H_, W_, LPB>(p, rng, mine, rev, fc, (int)cell64, J, S.row, lane, dgs, done, outcome, newly, total_rev,
+                        mines_changed, cell_rev);
+  DSTAMP(3);
   double reward = 0.0;
   if (outcome == MS_OUTCOME_LOSS) reward += p.loss_reward;
   if (outcome == MS_OUTCOME_WIN) reward += p.win_reward;
@@ -1244,96 +1375,14 @@ __global__ __launch_bounds__(64 * WPG) void k_step_packed(KParams p) {
     step_count = 0;
     mines_changed = true;
   }
-  PKSTAMP(4);
-
-  // ---- observation + action mask (env.py:172-196) of the wave's 4 boards. The obs are
-  // one-hot, so the wave zero-fills a byte image of them in LDS, each lane 16b+r sets the
-  // (at most two) 1 bytes of each revealed cell of row r, and the wave copies the image out
-  // as whole 1 KiB float4 stores (4 bytes -> 4 floats: v_cvt_f32_ubyte0..3) ----
-  if (p.obs || p.mask) {
-#pragma unroll
-    for (int k = 0; k < (IMG16 + kWave - 1) / kWave; ++k)
-      if (k * kWave + lane < IMG16) sImg_all[wv][k * kWave + lane] = make_uint4(0u, 0u, 0u, 0u);
-    const uint32_t m1 = mine << 1;
-    const uint32_t up1 = row_shr1(m1), dn1 = row_shl1(m1);  // rows r-1, r+1 (0 past the edge)
-    wave_sync();
-    if (r < H_) {
-      uint8_t* img = sImg + (lane / LPB) * (10 * A) + r * W_;
-      uint8_t* mk = sMask + (lane / LPB) * A + r * W_;
-#pragma unroll
-      for (int c = 0; c < W_; ++c) {
-        const uint32_t cnt = (uint32_t)__popc((up1 >> c) & 7u) + (uint32_t)__popc((dn1 >> c) & 7u) +
-                             ((m1 >> c) & 1u) + ((m1 >> (c + 2)) & 1u);
-        const uint32_t rv = (rev >> c) & 1u;
-        mk[c] = (uint8_t)(rv ^ 1u);
-        // unconditional byte stores, no branch per cell: channel 0 = revealed, channel 1 + count
-        // = 1 for a revealed cell after the first click (env.py:183-190); a hidden cell writes a
-        // 0 over the zero-filled byte of its channel 1 + count
-        img[c] = (uint8_t)rv;
-        img[(1 + cnt) * A + c] = (uint8_t)(fc ? rv : 0u);
-      }
-    }
-    PKSTAMP(8);
-    wave_sync();
-    const int nbl = (p.n - env0 < BPW) ? (int)(p.n - env0) : BPW;  // live boards of this wave
-    if (p.obs) {
-      float* ob = p.obs + env0 * 10 * A;
-      const uint32_t* s32 = reinterpret_cast<const uint32_t*>(sImg);
-      if (nbl == BPW) {
-        constexpr int NQ = BPW * 10 * A / 4;
-        float4* o4 = reinterpret_cast<float4*>(ob);
-#pragma unroll
-        for (int k = 0; k < (NQ + kWave - 1) / kWave; ++k) {
-          const int q = k * kWave + lane;
-          if (q < NQ) {
-            const uint32_t w = s32[q];
-            o4[q] = make_float4(ub2f<0>(w), ub2f<1>(w),
-                                ub2f<2>(w), ub2f<3>(w));
-          }
-        }
-      } else {  // partial last wave: whole float4s, then the odd tail floats
-        const int nf = nbl * 10 * A;
-        for (int q = lane; q < (nf >> 2); q += kWave) {
-          const uint32_t w = s32[q];
-          reinterpret_cast<float4*>(ob)[q] =
-              make_float4(ub2f<0>(w), ub2f<1>(w),
-                          ub2f<2>(w), ub2f<3>(w));
-        }
-        for (int f = (nf & ~3) + lane; f < nf; f += kWave) ob[f] = (float)sImg[f];
-      }
-    }
-    PKSTAMP(9);
-    if (p.mask) {
-      uint8_t* mb = p.mask + env0 * A;
-      const int nbytes = nbl * A;
-      if (BPW == 4) {  // env0 * A is a multiple of 4
-        for (int q = lane; q < (nbytes >> 2); q += kWave) reinterpret_cast<uint32_t*>(mb)[q] = sMask_all[wv][q];
-        for (int i = (nbytes & ~3) + lane; i < nbytes; i += kWave) mb[i] = sMask[i];
-      } else {  // a multiple of 2
-        const uint16_t* m16 = reinterpret_cast<const uint16_t*>(sMask);
-        for (int q = lane; q < (nbytes >> 1); q += kWave) reinterpret_cast<uint16_t*>(mb)[q] = m16[q];
-        if ((nbytes & 1) && lane == 0) mb[nbytes - 1] = sMask[nbytes - 1];
-      }
-    }
-  }
-  // ---- persist state: meta, then rows -> packed words through this wave's LDS ----
-  store_meta(mp, rng, step_count, fc, live ? r : 1);
-  const int rb = board_base<LPB>(lane);
-  sRow[lane] = mine;
-  sRev[lane] = rev;
-  wave_sync();
-  if (live && r < NW) {
-    uint64_t am = 0ull, ar_ = 0ull;
-#pragma unroll
-    for (int k = 0; k < RPW; ++k)
-      if (r * RPW + k < H_) {
-        am |= (uint64_t)sRow[rb + r * RPW + k] << (k * W_);
-        ar_ |= (uint64_t)sRev[rb + r * RPW + k] << (k * W_);
-      }
-    if (mines_changed) mwords[r] = am;
-    rwords[r] = ar_;
-  }
-  PKSTAMP(5);
+  DSTAMP(4);
+  const int nbl = (p.n - env0 < BPW) ? (int)(p.n - env0) : BPW;  // live boards of this wave
+  if (p.obs || p.mask)
+    pk_emit<H_, W_, BPW, LPB>(p.obs ? p.obs + env0 * 10 * A : nullptr, p.mask ? p.mask + env0 * A : nullptr, nbl,
+                              mine, rev, fc, S, lane, dgs);
+  pk_store_state<H_, W_, BPW, LPB>(p.meta + env, p.mine_words + env * NW, p.rev_words + env * NW, rng, step_count, fc,
+                                   mine, rev, mines_changed, live, S, lane);
+  DSTAMP(5);
 }
 
 // ---------------------------------------------------------------------------
@@ -1863,6 +1912,104 @@ __global__ __launch_bounds__(64 * EPW) void k_run(KParams p, RunParams r) {
   store_rows(rwords, rev, sR, g, lane);
 }
 
+// ms_run_tape on packed boards: k_run's T (tape, step) pairs per launch with k_step_packed's
+// layout (four boards per wave). The synthetic policy's k-th valid cell is found per board:
+// board sums and a DPP row scan over the board's 16 lanes, the board's bits of one ballot.
+__device__ __forceinline__ uint32_t row_excl_scan(uint32_t v) {  // inside one 16-lane DPP row
+  uint32_t s = v;
+  s += dpp32<0x111>(s);
+  s += dpp32<0x112>(s);
+  s += dpp32<0x114>(s);
+  s += dpp32<0x118>(s);
+  return s - v;
+}
+
+template <int H_, int W_, int LPB>
+__device__ __forceinline__ int pk_tape_cell(uint32_t mine, uint32_t rev, int lane, uint64_t gidx, uint64_t t, int mode) {
+  constexpr uint32_t ROWMASK = (1u << W_) - 1u;
+  constexpr uint64_t BM = (1ull << LPB) - 1ull;
+  const int r = lane & (LPB - 1);
+  const uint32_t valid = ~rev & ROWMASK & (r < H_ ? ~0u : 0u);
+  const uint64_t x = splitmix64(0xC0FFEEull ^ (gidx << 32) ^ t);
+  uint32_t bits = valid;
+  uint32_t cnt = board_sum<LPB>((uint32_t)__popc(valid), lane);
+  uint64_t sel = x;
+  if (mode == MS_TAPE_SAFE_BIASED) {  // (uniform branch: mode is a kernel argument)
+    const uint32_t safe = valid & ~mine;
+    const uint32_t n_safe = board_sum<LPB>((uint32_t)__popc(safe), lane);
+    sel = x >> 16;
+    if ((x & 0xFFFFull) < 65208ull && n_safe > 0) {
+      bits = safe;
+      cnt = n_safe;
+    }
+  }
+  const uint32_t target = mod64_small(sel, cnt ? cnt : 1u);
+  const uint32_t pc = (uint32_t)__popc(bits);
+  const uint32_t before = row_excl_scan(pc);
+  const bool hit = target >= before && target < before + pc;
+  const uint64_t who = (__ballot(hit) >> board_base<LPB>(lane)) & BM;
+  const int src = who ? __ffsll((unsigned long long)who) - 1 : 0;
+  const int col = (int)board_read<LPB>(hit ? (uint32_t)select_bit64(bits, target - before) : 0u, lane, src);
+  return cnt ? src * W_ + col : 0;
+}
+
+template <int H_, int W_, int WPG, int BPW>
+__global__ __launch_bounds__(64 * WPG) void k_run_packed(KParams p, RunParams rp) {
+  constexpr int LPB = kWave / BPW;
+  static_assert(BPW == 2 || BPW == 4, "boards per wave");
+  static_assert(packable<H_, W_>(), "packed board shape");
+  constexpr int A = H_ * W_;
+  constexpr int RPW = 64 / W_;
+  constexpr int NW = (H_ + RPW - 1) / RPW;
+  __shared__ PackedLds<H_, W_, BPW> S_all[WPG];
+  const int lane = lane_id();
+  const int r = lane & (LPB - 1);
+  const int wv = (WPG == 1) ? 0 : (int)rfl(threadIdx.x >> 6);
+  PackedLds<H_, W_, BPW>& S = S_all[wv];
+  const int64_t env0 = ((int64_t)blockIdx.x * WPG + wv) * BPW;
+  if (env0 >= p.n) return;  // (wave-uniform)
+  const int64_t env_raw = env0 + (lane / LPB);
+  const bool live = env_raw < p.n;
+  const int64_t env = live ? env_raw : p.n - 1;
+  uint32_t mine, rev;
+  uint64_t J[4];
+  Pcg rng;
+  int32_t step_count;
+  bool fc;
+  pk_load<H_, W_>(p, env, r, mine, rev, J, rng, step_count, fc);
+  const uint64_t gidx = (uint64_t)(rp.env_begin + env);
+  const int64_t n = p.n;
+  const int nbl = (n - env0 < BPW) ? (int)(n - env0) : BPW;
+  for (int t = 0; t < rp.T; ++t) {
+    const int64_t sbase = rp.slots ? (int64_t)t * n : 0;
+    const int cell = pk_tape_cell<H_, W_, LPB>(mine, rev, lane, gidx, rp.t0 + (uint64_t)t, rp.mode);
+    bool done, mines_changed = false, cell_rev;
+    int outcome;
+    uint32_t newly, total_rev;
+    pk_click<H_, W_, LPB>(p, rng, mine, rev, fc, cell, J, S.row, lane, nullptr, done, outcome, newly, total_rev,
+                          mines_changed, cell_rev);
+    double reward = 0.0;
+    if (outcome == MS_OUTCOME_LOSS) reward += p.loss_reward;
+    if (outcome == MS_OUTCOME_WIN) reward += p.win_reward;
+    reward -= p.step_penalty;
+    step_count += 1;
+    if (rp.actions && live && r == 0) rp.actions[sbase + env] = cell;
+    store_aux(p, sbase + env, live ? r : kWave, reward, done, step_count, newly, total_rev, outcome, A);
+    if (done) {  // auto-reset; the RNG continues
+      mine = 0u;
+      rev = 0u;
+      fc = false;
+      step_count = 0;
+    }
+    if (p.obs || p.mask)
+      pk_emit<H_, W_, BPW, LPB>(p.obs ? p.obs + (sbase + env0) * 10 * A : nullptr,
+                                p.mask ? p.mask + (sbase + env0) * A : nullptr, nbl, mine, rev, fc, S, lane, nullptr);
+    wave_sync();  // this step's LDS reads before the next step's placement / image writes
+  }
+  pk_store_state<H_, W_, BPW, LPB>(p.meta + env, p.mine_words + env * NW, p.rev_words + env * NW, rng, step_count, fc,
+                                   mine, rev, true, live, S, lane);
+}
+
 // ---------------------------------------------------------------------------
 // ms_gae: thread per env, reverse scan over T, reference f32 op order
 // (buffers.py:87-94) with explicit round-to-nearest ops (no contraction).
@@ -2139,6 +2286,23 @@ void launch_step(const KParams& p, int epw, hipStream_t s, hipEvent_t ev0, hipEv
 
 template <int H_, int W_>
 void launch_run(const KParams& p, const RunParams& r, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+  if constexpr (packable<H_, W_>()) {
+    // small boards: four per wave (k_run_packed); each step's 4-board obs / mask chunk must
+    // start 16-B / 4-B aligned, in every slot
+    const bool slot_ok = !r.slots || ((p.n * H_ * W_) & 3) == 0;
+    if (p.K >= 1 && p.K <= 16 && !(p.dbg_flags & (MS_DBG_ONE_BOARD_PER_WAVE | MS_DBG_FORCE_CHAIN_PLACEMENT)) &&
+        ((uintptr_t)p.obs & 15u) == 0 && ((uintptr_t)p.mask & 3u) == 0 && slot_ok) {
+      constexpr int WPG = 4;
+      if (p.dbg_flags & MS_DBG_TWO_BOARDS_PER_WAVE) {
+        const unsigned grid = (unsigned)((p.n + 2 * WPG - 1) / (2 * WPG));
+        hipExtLaunchKernelGGL((k_run_packed<H_, W_, WPG, 2>), dim3(grid), dim3(64 * WPG), 0, s, ev0, ev1, 0, p, r);
+      } else {
+        const unsigned grid = (unsigned)((p.n + 4 * WPG - 1) / (4 * WPG));
+        hipExtLaunchKernelGGL((k_run_packed<H_, W_, WPG, 4>), dim3(grid), dim3(64 * WPG), 0, s, ev0, ev1, 0, p, r);
+      }
+      return;
+    }
+  }
   if (H_ && W_)
     hipExtLaunchKernelGGL((k_run<H_, W_, 4>), dim3((unsigned)((p.n + 3) / 4)), dim3(256), 0, s, ev0, ev1, 0, p, r);
   else hipExtLaunchKernelGGL((k_run<H_, W_, 1>), dim3((unsigned)p.n), dim3(64), 0, s, ev0, ev1, 0, p, r);

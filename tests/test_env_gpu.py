@@ -357,6 +357,32 @@ def test_run_tape_equals_step_loop(gpu, H, W, K, mode):
         assert torch.equal(sa[k], sb[k]), k
 
 
+@pytest.mark.parametrize("H,W,K,N,slots", [(9, 9, 10, 300, True), (9, 9, 10, 203, False), (8, 8, 10, 130, True),
+                                           (9, 9, 16, 64, True)])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_run_tape_packed_equals_one_board_per_wave(gpu, H, W, K, N, slots, mode):
+    """k_run_packed (four boards per wave; two with MS_DBG_TWO_BOARDS_PER_WAVE) is bit-exact
+    with k_run (one board per wave) over two launches: every output slot, the boards and the
+    RNG state; N = 203 / 130 leave a partial last wave."""
+    from ms_amd import _lib as L
+    vs = [_vec(H, W, K, N, seed=13) for _ in range(3)]
+    vs[1].set_debug_flags(L.MS_DBG_ONE_BOARD_PER_WAVE)
+    vs[2].set_debug_flags(L.MS_DBG_TWO_BOARDS_PER_WAVE)
+    for v in vs:
+        v.reset()
+    for t0 in (5, 40):
+        outs = [v.run_tape(t0, 35, mode, slots=slots) for v in vs]
+        for o in outs[1:]:
+            for k in _RUN_KEYS:
+                assert torch.equal(outs[0][k], o[k]), (t0, k)
+    st = vs[0].rng_state()
+    assert all(np.array_equal(st, v.rng_state()) for v in vs[1:])
+    snaps = [v.snapshot_tensors() for v in vs]
+    for sn in snaps[1:]:
+        for k in snaps[0]:
+            assert torch.equal(snaps[0][k], sn[k]), k
+
+
 def test_run_tape_sharded_and_late_start(gpu):
     from ms_amd import EnvConfig, VecMinesweeper
     from ms_amd._lib import MsEnvError

@@ -41,12 +41,13 @@ def grid_threads(r):
 disp = defaultdict(list)  # (kernel tag, board, grid threads) -> [(start, dur_ns)]
 for r in rows:
     name = r["Kernel_Name"]
-    # k_step_packed (four small boards per wave) is the k_step of 9x9 / 8x8 boards
-    for tag, pat in (("k_step", "k_step<"), ("k_step", "k_step_packed<"), ("k_run", "k_run<")):
+    # k_step_packed / k_run_packed (four small boards per wave) are k_step / k_run of 9x9 / 8x8
+    for tag, pat in (("k_step", "k_step<"), ("k_step", "k_step_packed<"), ("k_run", "k_run<"),
+                     ("k_run", "k_run_packed<")):
         if pat in name:
             board = name.split(pat, 1)[1].split(">", 1)[0].split(",")[:2]
             g = grid_threads(r)
-            if pat == "k_step_packed<":
+            if pat in ("k_step_packed<", "k_run_packed<"):
                 g *= 4  # 16 boards per 256-thread workgroup -> the same key as 64 lanes per board
             key = (tag, f"{int(board[0])}x{int(board[1])}", g)
             disp[key].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))

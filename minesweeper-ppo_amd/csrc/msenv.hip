@@ -526,14 +526,19 @@ __device__ __forceinline__ uint32_t bperm(uint32_t v, int src_lane) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
 }
 
-// Fully lane-parallel placement for 1 <= K <= 128 (every benchmark board):
-// the <= 128 PCG64 outputs come from two jump-ahead chunks, lane i (and i+64)
-// owns Floyd iteration i, and Floyd's sequential "t already chosen -> take j"
-// rule is solved as a fixpoint: sel_i = c_i unless some earlier sel equals
-// c_i, iterated until nothing changes (the sequential answer is the unique
-// fixpoint; collision chains are short, ~2-4 rounds). Set membership uses a
-// round-tagged LDS table indexed by cell. Returns false on a Lemire rejection
-// (caller falls back to place_serial), leaving rng untouched.
+// Fully lane-parallel placement for 1 <= K <= 128 (every benchmark board): the <= 128
+// PCG64 outputs come from two jump-ahead chunks, and lane i (and i+64) owns Floyd iteration
+// i: j_i = pop-K+i, t_i = its bounded draw in [0, j_i]. Floyd inserts t_i unless it is
+// already chosen, then j_i. The j are distinct and larger than every earlier choice, so "t_i
+// already chosen" has a closed form: t_i equals an earlier t_k (chosen either way: as itself
+// or because it already was), or t_i equals j_k for the one k = t_i - (pop-K) < i whose own
+// t_k collided. The first term is one LDS atomicMin per iteration into a table indexed by t
+// (t_i repeats an earlier draw iff the table's minimum is not i); the second follows k by
+// ds_bpermute until nothing changes (chains are short: 1-2 rounds). Returns false on a
+// Lemire rejection (the caller falls back to place_serial), leaving rng untouched.
+__device__ __forceinline__ bool lemire_maybe(uint32_t left, uint32_t bound) {  // a rejection is possible
+  return left < bound + 1u;
+}
 // MS_DIAG builds: sub-phase stamps of a placement (diag slots 8..13 of the env)
 #ifdef MS_DIAG
 #define PSTAMP(k)                                                  \
@@ -564,11 +569,19 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
   Out o1 = o0;
   if (n_out > 64) o1 = jump_out(readlane64(o0.sh, 63), readlane64(o0.sl, 63), J[0], J[1], ci_hi, ci_lo);
   PSTAMP(9);
-  // Lemire rejection test of every consumed draw (draw p of output q, half hf)
-  bool rej = false;
+  // Lemire rejection test of every consumed draw (draw p of output q, half hf). A draw can
+  // only be rejected if its leftover is below bound + 1, which almost never happens: the
+  // exact test (a 32-bit remainder) runs only in a wave where some draw is that low.
+  uint32_t lft[5], bnd[5];
+  bool maybe = false;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    lft[k] = 0xffffffffu;
+    bnd[k] = 0u;
+  }
   if (h0 && D > 0) {
-    const uint32_t bound = (nF > 0) ? (uint32_t)(pop - K + z0) : (uint32_t)(K - 1);
-    rej |= lemire_rejects((uint32_t)((uint64_t)rng.uinteger * (bound + 1u)), bound);
+    bnd[4] = (nF > 0) ? (uint32_t)(pop - K + z0) : (uint32_t)(K - 1);
+    lft[4] = (uint32_t)((uint64_t)rng.uinteger * (bnd[4] + 1u));
   }
 #pragma unroll
   for (int ch = 0; ch < 2; ++ch) {
@@ -579,21 +592,28 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
       const int pidx = h0 + 2 * (q - 1) + hf;
       if (q <= n_out && pidx < D) {
         const uint32_t d = hf ? (uint32_t)(x >> 32) : (uint32_t)x;
-        const uint32_t bound = pidx < nF ? (uint32_t)(pop - K + z0 + pidx) : (uint32_t)(K - 1 - (pidx - nF));
-        rej |= lemire_rejects((uint32_t)((uint64_t)d * (bound + 1u)), bound);
+        bnd[2 * ch + hf] = pidx < nF ? (uint32_t)(pop - K + z0 + pidx) : (uint32_t)(K - 1 - (pidx - nF));
+        lft[2 * ch + hf] = (uint32_t)((uint64_t)d * (bnd[2 * ch + hf] + 1u));
       }
     }
   }
-  if (__ballot(rej) != 0ull) return false;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) maybe |= lemire_maybe(lft[k], bnd[k]);
+  if (__ballot(maybe) != 0ull) {  // (uniform, rare) the exact test
+    bool rej = false;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) rej |= lemire_rejects(lft[k], bnd[k]);
+    if (__ballot(rej) != 0ull) return false;
+  }
   PSTAMP(10);
-  // Floyd candidates: lane owns iterations i = lane + 64 s
-  int cand[2], alt[2], sel[2];
+  // Floyd draws: lane owns iterations i = lane + 64 s
+  int t[2], jj[2];
   bool valid[2];
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2) {
     const int i = lane + 64 * s2;
     valid[s2] = i < K;
-    const int j = pop - K + i;
+    jj[s2] = pop - K + i;
     const int pidx = i - z0;
     const int idx = pidx - h0;
     // ds_bpermute delivers the SOURCE lane's register: fetch both halves of both
@@ -603,44 +623,56 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
     const uint32_t w1l = bperm((uint32_t)o1.x, src), w1h = bperm((uint32_t)(o1.x >> 32), src);
     uint32_t d = (idx >> 7) ? ((idx & 1) ? w1h : w1l) : ((idx & 1) ? w0h : w0l);
     if (h0 && pidx == 0) d = rng.uinteger;
-    const uint32_t t = (i >= z0) ? (uint32_t)(((uint64_t)d * (uint32_t)(j + 1)) >> 32) : 0u;
-    cand[s2] = map_allowed((int)t, F.f, F.m);
-    alt[s2] = map_allowed(j, F.f, F.m);
-    sel[s2] = cand[s2];
+    t[s2] = (i >= z0) ? (int)(((uint64_t)d * (uint32_t)(jj[s2] + 1)) >> 32) : 0;
   }
-  for (int c = lane; c < A; c += kWave) tab[c] = 0u;
+  for (int c = lane; c < A; c += kWave) tab[c] = 0xffffffffu;
   wave_sync();
   PSTAMP(11);
-  for (uint32_t round = 1; round <= (uint32_t)K + 1; ++round) {
-#ifdef MS_DIAG
-    if (dg && lane == 0) dg[14] = round;
-#endif
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-      if (valid[s2]) atomicMax(&tab[sel[s2]], (round << 16) | (0xFFFFu - (uint32_t)(lane + 64 * s2)));
-    wave_sync();
+  for (int s2 = 0; s2 < 2; ++s2)
+    if (valid[s2]) atomicMin(&tab[t[s2]], (uint32_t)(lane + 64 * s2));
+  wave_sync();
+  bool dup[2], col[2], kv[2];
+  int ks[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const int i = lane + 64 * s2;
+    dup[s2] = valid[s2] && tab[t[s2]] != (uint32_t)i;
+    ks[s2] = t[s2] - (pop - K);  // t_i == j_ks
+    kv[s2] = valid[s2] && ks[s2] >= 0 && ks[s2] < i;
+    col[s2] = dup[s2];
+  }
+  uint32_t rounds = 0;
+  while (true) {
+    ++rounds;
     bool changed = false;
+    bool nc[2];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      if (valid[s2]) {
-        const uint32_t e = tab[cand[s2]];
-        const bool coll = (e >> 16) == round && (0xFFFFu - (e & 0xFFFFu)) < (uint32_t)(lane + 64 * s2);
-        const int nv = coll ? alt[s2] : cand[s2];
-        changed |= nv != sel[s2];
-        sel[s2] = nv;
-      }
+      // every lane takes part in both reads (ds_bpermute returns 0 from an EXEC-disabled lane)
+      const int src = ks[s2] & 63;
+      const uint32_t c0 = bperm(col[0] ? 1u : 0u, src), c1 = bperm(col[1] ? 1u : 0u, src);
+      nc[s2] = dup[s2] || (kv[s2] && ((ks[s2] >= 64 ? c1 : c0) != 0u));
+      changed |= nc[s2] != col[s2];
     }
-    wave_sync();
+    col[0] = nc[0];
+    col[1] = nc[1];
     if (__ballot(changed) == 0ull) break;
   }
+#ifdef MS_DIAG
+  if (dg && lane == 0) dg[14] = rounds;
+#else
+  (void)rounds;
+#endif
   PSTAMP(12);
   srow[lane] = 0ull;
   wave_sync();
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2)
     if (valid[s2]) {
-      const int r = sel[s2] / W;
-      atomicOr((unsigned long long*)&srow[r], 1ull << (sel[s2] - r * W));
+      const int cell = map_allowed(col[s2] ? jj[s2] : t[s2], F.f, F.m);
+      const int r = cell / W;
+      atomicOr((unsigned long long*)&srow[r], 1ull << (cell - r * W));
     }
   wave_sync();
   mine_out = lane < g.H ? srow[lane] : 0ull;
@@ -1017,21 +1049,27 @@ __device__ bool place_packed(Pcg& rng, uint32_t& mine_out, const Block& B, int K
   const uint64_t ci_lo = J[3] * rng.ilo;
   const uint64_t ci_hi = __umul64hi(J[3], rng.ilo) + J[3] * rng.ihi + J[2] * rng.ilo;
   const Out o = jump_out(rng.hi, rng.lo, J[0], J[1], ci_hi, ci_lo);
-  bool rej = false;
+  // Lemire rejection test of the board's draws; the exact test (a 32-bit remainder) runs only
+  // in a wave where some leftover is below its bound + 1 (place_fixpoint)
+  uint32_t lft[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, bnd[3] = {0u, 0u, 0u};
   if (h0 && D > 0) {
-    const uint32_t bound = (nF > 0) ? (uint32_t)(pop - K + z0) : (uint32_t)(K - 1);
-    rej |= lemire_rejects((uint32_t)((uint64_t)rng.uinteger * (bound + 1u)), bound);
+    bnd[2] = (nF > 0) ? (uint32_t)(pop - K + z0) : (uint32_t)(K - 1);
+    lft[2] = (uint32_t)((uint64_t)rng.uinteger * (bnd[2] + 1u));
   }
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf) {
     const int pidx = h0 + 2 * r + hf;
     if (r < n_out && pidx < D) {
       const uint32_t d = hf ? (uint32_t)(o.x >> 32) : (uint32_t)o.x;
-      const uint32_t bound = pidx < nF ? (uint32_t)(pop - K + z0 + pidx) : (uint32_t)(K - 1 - (pidx - nF));
-      rej |= lemire_rejects((uint32_t)((uint64_t)d * (bound + 1u)), bound);
+      bnd[hf] = pidx < nF ? (uint32_t)(pop - K + z0 + pidx) : (uint32_t)(K - 1 - (pidx - nF));
+      lft[hf] = (uint32_t)((uint64_t)d * (bnd[hf] + 1u));
     }
   }
-  if (board_any<LPB>(rej, lane)) return false;
+  const bool maybe = lemire_maybe(lft[0], bnd[0]) || lemire_maybe(lft[1], bnd[1]) || lemire_maybe(lft[2], bnd[2]);
+  if (__ballot(maybe) != 0ull) {
+    const bool rej = lemire_rejects(lft[0], bnd[0]) || lemire_rejects(lft[1], bnd[1]) || lemire_rejects(lft[2], bnd[2]);
+    if (board_any<LPB>(rej, lane)) return false;
+  }
   QSTAMP(10);
   // lane r: Floyd iteration i = r (draw pidx = i - z0, from output (pidx - h0) / 2)
   const int jr = pop - K + r;

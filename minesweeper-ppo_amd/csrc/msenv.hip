@@ -402,6 +402,43 @@ __device__ __forceinline__ void floyd_insert(uint64_t& mine, int c1, int j, cons
   if (lane == r1) mine |= 1ull << col;
 }
 
+// The forbidden cells of a placement (env.py:280-307) as a block: nr rows of nc cells from
+// cell base0 (the click's clipped 3x3 neighbourhood, or the click alone: nr = nc = 1).
+struct Block {
+  int base0, nr, nc, pop;
+};
+template <int H_, int W_>
+__device__ __forceinline__ Block make_block(int cell, int ar, int ac, int K, bool guarantee) {
+  Block B;
+  if (guarantee) {
+    const int r0 = ar > 0 ? ar - 1 : 0, r1 = ar < H_ - 1 ? ar + 1 : H_ - 1;
+    const int c0 = ac > 0 ? ac - 1 : 0, c1 = ac < W_ - 1 ? ac + 1 : W_ - 1;
+    B.base0 = r0 * W_ + c0;
+    B.nr = r1 - r0 + 1;
+    B.nc = c1 - c0 + 1;
+  } else {
+    B.base0 = cell;
+    B.nr = B.nc = 1;
+  }
+  B.pop = H_ * W_ - B.nr * B.nc;
+  if (B.pop < K) {  // env.py:303-307: relax to the clicked cell only
+    B.base0 = cell;
+    B.nr = B.nc = 1;
+    B.pop = H_ * W_ - 1;
+  }
+  return B;
+}
+// allowed index t -> cell (numpy's flatnonzero(~forbidden)[t], env.py:302), closed form:
+// past base0 the allowed cells come in gaps of W - nc between the block's row runs.
+template <int W_>
+__device__ __forceinline__ int map_block(int t, const Block& B) {
+  static_assert(W_ > 3, "a 3-wide block must leave a gap in every row");
+  if (t < B.base0) return t;
+  const int tp = t - B.base0;
+  const int q = B.nc == 3 ? tp / (W_ - 3) : (B.nc == 2 ? tp / (W_ - 2) : tp / (W_ - 1));
+  return B.base0 + tp + B.nc * (1 + (q < B.nr - 1 ? q : B.nr - 1));
+}
+
 // Serial reference-order placement (also the fallback of the parallel one).
 template <int H_, int W_>
 __device__ void place_serial(Pcg& rng, uint64_t& mine, const Forbid& F, int K, const Geo<H_, W_>& g, int lane) {
@@ -549,10 +586,13 @@ __device__ __forceinline__ bool lemire_maybe(uint32_t left, uint32_t bound) {  /
 #define PSTAMP(k) do { } while (0)
 #endif
 
-template <int H_, int W_>
-__device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, int K, const uint64_t (&J)[4],
-                               uint32_t* tab, uint64_t* srow, const Geo<H_, W_>& g, int lane,
+// NS = iteration slots per lane: 1 for K <= 64 (one jump-ahead chunk), 2 for K <= 128.
+// Compile-time shapes with W > 3 map allowed indices to cells in closed form (map_block).
+template <int H_, int W_, int NS>
+__device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, const Block& B, int K,
+                               const uint64_t (&J)[4], uint32_t* tab, uint64_t* srow, const Geo<H_, W_>& g, int lane,
                                uint64_t* dg = nullptr) {
+  (void)B;
   (void)dg;
   PSTAMP(8);
   const int A = g.A(), W = g.W;
@@ -567,7 +607,7 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
   const uint64_t ci_hi = __umul64hi(J[3], rng.ilo) + J[3] * rng.ihi + J[2] * rng.ilo;
   const Out o0 = jump_out(rng.hi, rng.lo, J[0], J[1], ci_hi, ci_lo);
   Out o1 = o0;
-  if (n_out > 64) o1 = jump_out(readlane64(o0.sh, 63), readlane64(o0.sl, 63), J[0], J[1], ci_hi, ci_lo);
+  if (NS == 2 && n_out > 64) o1 = jump_out(readlane64(o0.sh, 63), readlane64(o0.sl, 63), J[0], J[1], ci_hi, ci_lo);
   PSTAMP(9);
   // Lemire rejection test of every consumed draw (draw p of output q, half hf). A draw can
   // only be rejected if its leftover is below bound + 1, which almost never happens: the
@@ -584,7 +624,7 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
     lft[4] = (uint32_t)((uint64_t)rng.uinteger * (bnd[4] + 1u));
   }
 #pragma unroll
-  for (int ch = 0; ch < 2; ++ch) {
+  for (int ch = 0; ch < NS; ++ch) {
     const uint64_t x = ch ? o1.x : o0.x;
     const int q = 64 * ch + lane + 1;
 #pragma unroll
@@ -607,10 +647,10 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
   }
   PSTAMP(10);
   // Floyd draws: lane owns iterations i = lane + 64 s
-  int t[2], jj[2];
-  bool valid[2];
+  int t[NS], jj[NS];
+  bool valid[NS];
 #pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) {
+  for (int s2 = 0; s2 < NS; ++s2) {
     const int i = lane + 64 * s2;
     valid[s2] = i < K;
     jj[s2] = pop - K + i;
@@ -620,8 +660,11 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
     // chunks in converged control flow, then select by this lane's idx
     const int src = (idx >> 1) & 63;
     const uint32_t w0l = bperm((uint32_t)o0.x, src), w0h = bperm((uint32_t)(o0.x >> 32), src);
-    const uint32_t w1l = bperm((uint32_t)o1.x, src), w1h = bperm((uint32_t)(o1.x >> 32), src);
-    uint32_t d = (idx >> 7) ? ((idx & 1) ? w1h : w1l) : ((idx & 1) ? w0h : w0l);
+    uint32_t d = (idx & 1) ? w0h : w0l;
+    if (NS == 2) {
+      const uint32_t w1l = bperm((uint32_t)o1.x, src), w1h = bperm((uint32_t)(o1.x >> 32), src);
+      if (idx >> 7) d = (idx & 1) ? w1h : w1l;
+    }
     if (h0 && pidx == 0) d = rng.uinteger;
     t[s2] = (i >= z0) ? (int)(((uint64_t)d * (uint32_t)(jj[s2] + 1)) >> 32) : 0;
   }
@@ -629,13 +672,13 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
   wave_sync();
   PSTAMP(11);
 #pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2)
+  for (int s2 = 0; s2 < NS; ++s2)
     if (valid[s2]) atomicMin(&tab[t[s2]], (uint32_t)(lane + 64 * s2));
   wave_sync();
-  bool dup[2], col[2], kv[2];
-  int ks[2];
+  bool dup[NS], col[NS], kv[NS];
+  int ks[NS];
 #pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) {
+  for (int s2 = 0; s2 < NS; ++s2) {
     const int i = lane + 64 * s2;
     dup[s2] = valid[s2] && tab[t[s2]] != (uint32_t)i;
     ks[s2] = t[s2] - (pop - K);  // t_i == j_ks
@@ -646,17 +689,18 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
   while (true) {
     ++rounds;
     bool changed = false;
-    bool nc[2];
+    bool nc[NS];
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      // every lane takes part in both reads (ds_bpermute returns 0 from an EXEC-disabled lane)
+    for (int s2 = 0; s2 < NS; ++s2) {
+      // every lane takes part in the reads (ds_bpermute returns 0 from an EXEC-disabled lane)
       const int src = ks[s2] & 63;
-      const uint32_t c0 = bperm(col[0] ? 1u : 0u, src), c1 = bperm(col[1] ? 1u : 0u, src);
+      const uint32_t c0 = bperm(col[0] ? 1u : 0u, src);
+      const uint32_t c1 = NS == 2 ? bperm(col[NS - 1] ? 1u : 0u, src) : 0u;
       nc[s2] = dup[s2] || (kv[s2] && ((ks[s2] >= 64 ? c1 : c0) != 0u));
       changed |= nc[s2] != col[s2];
     }
-    col[0] = nc[0];
-    col[1] = nc[1];
+#pragma unroll
+    for (int s2 = 0; s2 < NS; ++s2) col[s2] = nc[s2];
     if (__ballot(changed) == 0ull) break;
   }
 #ifdef MS_DIAG
@@ -668,9 +712,11 @@ __device__ bool place_fixpoint(Pcg& rng, uint64_t& mine_out, const Forbid& F, in
   srow[lane] = 0ull;
   wave_sync();
 #pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2)
+  for (int s2 = 0; s2 < NS; ++s2)
     if (valid[s2]) {
-      const int cell = map_allowed(col[s2] ? jj[s2] : t[s2], F.f, F.m);
+      int cell;
+      if constexpr (W_ > 3) cell = map_block<W_>(col[s2] ? jj[s2] : t[s2], B);
+      else cell = map_allowed(col[s2] ? jj[s2] : t[s2], F.f, F.m);
       const int r = cell / W;
       atomicOr((unsigned long long*)&srow[r], 1ull << (cell - r * W));
     }
@@ -730,13 +776,17 @@ __device__ __forceinline__ void board_click(Pcg& rng, uint64_t& mine, uint64_t& 
       const Forbid F = make_forbid(cell, ar, ac, p.K, p.guarantee != 0, g);
       bool ok = false;
       if (!(p.dbg_flags & MS_DBG_FORCE_SERIAL_PLACEMENT)) {
-        if (p.K >= 1 && p.K <= 128 && !(p.dbg_flags & MS_DBG_FORCE_CHAIN_PLACEMENT))
+        if (p.K >= 1 && p.K <= 128 && !(p.dbg_flags & MS_DBG_FORCE_CHAIN_PLACEMENT)) {
+          Block B{};
+          if constexpr (W_ > 3) B = make_block<H_, W_>(cell, ar, ac, p.K, p.guarantee != 0);
 #ifdef MS_DIAG
-          ok = place_fixpoint(rng, mine, F, p.K, J, sTab, sR, g, lane,
-                              (p.diag && env >= 0) ? p.diag + env * 16 : nullptr);
+          uint64_t* dgp = (p.diag && env >= 0) ? p.diag + env * 16 : nullptr;
 #else
-          ok = place_fixpoint(rng, mine, F, p.K, J, sTab, sR, g, lane);
+          uint64_t* dgp = nullptr;
 #endif
+          ok = p.K <= 64 ? place_fixpoint<H_, W_, 1>(rng, mine, F, B, p.K, J, sTab, sR, g, lane, dgp)
+                         : place_fixpoint<H_, W_, 2>(rng, mine, F, B, p.K, J, sTab, sR, g, lane, dgp);
+        }
         else
           ok = place_parallel(rng, mine, F, p.K, J, g, lane);
       }
@@ -976,43 +1026,6 @@ __device__ __forceinline__ void set_add(uint64_t& s0, uint64_t& s1, uint32_t c) 
   const uint64_t bit = 1ull << (c & 63u);
   if (c < 64u) s0 |= bit;
   else s1 |= bit;
-}
-
-// The forbidden cells of a placement (env.py:280-307) as a block: nr rows of nc cells from
-// cell base0 (the click's clipped 3x3 neighbourhood, or the click alone: nr = nc = 1).
-struct Block {
-  int base0, nr, nc, pop;
-};
-template <int H_, int W_>
-__device__ __forceinline__ Block make_block(int cell, int ar, int ac, int K, bool guarantee) {
-  Block B;
-  if (guarantee) {
-    const int r0 = ar > 0 ? ar - 1 : 0, r1 = ar < H_ - 1 ? ar + 1 : H_ - 1;
-    const int c0 = ac > 0 ? ac - 1 : 0, c1 = ac < W_ - 1 ? ac + 1 : W_ - 1;
-    B.base0 = r0 * W_ + c0;
-    B.nr = r1 - r0 + 1;
-    B.nc = c1 - c0 + 1;
-  } else {
-    B.base0 = cell;
-    B.nr = B.nc = 1;
-  }
-  B.pop = H_ * W_ - B.nr * B.nc;
-  if (B.pop < K) {  // env.py:303-307: relax to the clicked cell only
-    B.base0 = cell;
-    B.nr = B.nc = 1;
-    B.pop = H_ * W_ - 1;
-  }
-  return B;
-}
-// allowed index t -> cell (numpy's flatnonzero(~forbidden)[t], env.py:302), closed form:
-// past base0 the allowed cells come in gaps of W - nc between the block's row runs.
-template <int W_>
-__device__ __forceinline__ int map_block(int t, const Block& B) {
-  static_assert(W_ > 3, "a 3-wide block must leave a gap in every row");
-  if (t < B.base0) return t;
-  const int tp = t - B.base0;
-  const int q = B.nc == 3 ? tp / (W_ - 3) : (B.nc == 2 ? tp / (W_ - 2) : tp / (W_ - 1));
-  return B.base0 + tp + B.nc * (1 + (q < B.nr - 1 ? q : B.nr - 1));
 }
 
 // Placement of one packed board (same draws and result as place_fixpoint). The <= 16

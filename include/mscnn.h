@@ -72,7 +72,8 @@ int mc_heads_fwd(const uint16_t* f, const uint16_t* w1, const float* b1, const f
                  float* out_p, float* out_m, int64_t M, int32_t dtype, void* stream);
 
 /* Backward of both heads. dlp/dlm: f32 [M] logit gradients (dlm may be NULL = 0).
- * w1pT: bf16 [96][96] = policy W1 transposed. df (bf16 [M][96]) = policy-head input
+ * w1pT: ignored, may be NULL (round 2's policy W1^T copy; the kernel now reads W1 transposed
+ * from its own LDS image). df (bf16 [M][96]) = policy-head input
  * gradient (the mine head reads f.detach()) + gadd[m / P] (f32 [M/P][96], may be NULL).
  * dw1: f32 [192][96], db1, dw2: f32 [192]. work: mc_heads_bwd_workspace(M) floats. */
 int mc_heads_bwd(const uint16_t* f, const float* dlp, const float* dlm, const uint16_t* w1, const uint16_t* w1pT,

@@ -11,9 +11,11 @@
 //   rows from LDS, B = f rows loaded straight from HBM), bias + ReLU + the w2 dot
 //   product in registers (the channel sum is in-lane plus one lane^32 add), one f32
 //   logit per row and head. f is read once for both heads; h never reaches HBM.
-// k_heads_bwd: per 128-row tile, recompute H[px][c] (A = f tile in LDS, B = W1),
+// k_heads_bwd: per 64-row tile (two workgroups per CU: 78.8 KB of LDS each), recompute
+//   H[px][c] (A = f tile in LDS, B = W1),
 //   dh = dlogit * w2 * (h > 0) written to an LDS image (bf16), then
-//     df^T = W1p^T . dh_p^T  (policy only: the mine head sees f.detach()),
+//     df^T = W1p^T . dh_p^T  (policy only: the mine head sees f.detach(); W1p^T read from
+//                             the W1 image with ds_read_b64_tr_b16),
 //     dW1 += dh^T . f        (K = the tile's pixels; both operands K-major via
 //                             ds_read_b64_tr_b16 from the LDS images),
 //     dw2 += h^T . dlogit, db1 += sum dh  (in-lane accumulators);
@@ -131,7 +133,7 @@ struct HeadBwdParams {
   const float* dlp;
   const float* dlm;
   const E* w1;   // [192][96]
-  const E* w1pT; // [96 k][96 c] policy W1 transposed
+  const E* w1pT; // unused (round 2's policy W1^T copy)
   const float* b1;
   const float* w2;
   const float* gadd;  // [M / P][96] or null: added to df (the value head's pooled gradient / P)
@@ -150,43 +152,43 @@ __device__ __forceinline__ int sd_off(int r, int col) {
   return r * NH + 8 * ((col >> 3) ^ ((((r >> 1) & 1) << 2) | ((r >> 2) & 3))) + (col & 7);
 }
 
+// k_heads_bwd LDS (78.8 KB: two workgroups per CU). 64-row tiles; the policy W1^T operand
+// of df is read from the W1 image by transposing LDS reads, so no W1^T copy is kept.
+constexpr int TRB = 64;  // rows per backward tile
 template <typename E>
 struct HeadLds {
   E w[NH * WP];     // W1 rows [c][k]
-  E wt[C * WP];     // policy W1^T rows [k][c]
-  E f[TR * C];      // swizzled f tile
-  E dh[TR * NH];    // swizzled dh image
-  E df[TR * C];     // df rows, each wave's 32 rows staged for contiguous 16-B stores
-  float dl[2][TR];
+  E f[TRB * C];     // swizzled f tile
+  E dh[TRB * NH];   // swizzled dh image; after the tile loop: the dw2 / db1 combine
+  float dl[2][TRB];
   float b1[NH], w2[NH];
-  float red[2][NH];
 };
+static_assert(sizeof(HeadLds<__bf16>) <= 80 * 1024, "two k_heads_bwd workgroups per CU");
 
-template <typename E, int T0, int NTW>
+// one wave's share of a 64-row tile: H recompute for px-tile pt (wave & 1) and head hd
+// (wave >> 1: 0 policy, 1 mine), its dh columns, df for px-tile pt and k-tiles [KT0, KT0+NKT),
+// and dW1 tiles [T0, T0+NTW) of the 18 (6 c-tiles x 3 k-tiles)
+template <typename E, int T0, int NTW, int KT0, int NKT>
 __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLds<E>& L) {
   typedef typename EV<E>::v8 E8;
-  typedef typename EV<E>::v4 E4;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hh = lane >> 5;
   const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int pt = wave & 1, hd = wave >> 1;
   f32x16 dwacc[NTW];
 #pragma unroll
   for (int t = 0; t < NTW; ++t)
 #pragma unroll
     for (int i = 0; i < 16; ++i) dwacc[t][i] = 0.f;
-  float dw2acc[6], db1acc[6];
+  float dw2acc[3], db1acc[3];
 #pragma unroll
-  for (int ct = 0; ct < 6; ++ct) dw2acc[ct] = db1acc[ct] = 0.f;
+  for (int j = 0; j < 3; ++j) dw2acc[j] = db1acc[j] = 0.f;
 
-  const int64_t ntiles = (p.M + TR - 1) / TR;
-  constexpr int NFC = TR * 12 / 256;
+  const int64_t ntiles = (p.M + TRB - 1) / TRB;
+  constexpr int NFC = TRB * 12 / 256;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int64_t base = tile * TR;
+    const int64_t base = tile * TRB;
     const int zo = opaque0();
-    // ---- stage f tile and the two logit gradients ----
-    // (prefetching the next tile here needs ~26 more VGPRs than the kernel has: spills)
-    // every load is issued unconditionally from a clamped row and masked afterwards:
-    // a guarded load sits in its own exec branch with its own vmcnt(0), one round
-    // trip per chunk
+    // ---- stage f tile and the two logit gradients (unconditional loads from clamped rows) ----
     {
       u32x4 v[NFC];
 #pragma unroll
@@ -195,7 +197,7 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
         const int64_t row = base + r < p.M ? base + r : p.M - 1;
         v[i] = *reinterpret_cast<const u32x4*>(&p.f[row * C + ch * 8]);
       }
-      const int64_t rowd = base + (tid & (TR - 1)) < p.M ? base + (tid & (TR - 1)) : p.M - 1;
+      const int64_t rowd = base + (tid & (TRB - 1)) < p.M ? base + (tid & (TRB - 1)) : p.M - 1;
       const float d0 = p.dlp[rowd];
       const float d1 = p.dlm ? p.dlm[rowd] : 0.f;
 #pragma unroll
@@ -204,108 +206,100 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
         if (base + r >= p.M) v[i] = u32x4{0u, 0u, 0u, 0u};
         *reinterpret_cast<u32x4*>(&L.f[sf_off(r, ch * 8)]) = v[i];
       }
-      if (tid < TR) {
+      if (tid < TRB) {
         const bool ok = base + tid < p.M;
         L.dl[0][tid] = ok ? d0 : 0.f;
         L.dl[1][tid] = ok ? d1 : 0.f;
       }
     }
     __syncthreads();
-    // ---- recompute H[px][c] for this wave's 32 rows ----
+    // ---- recompute H[px][c] for px-tile pt and this head's three c-tiles; dh -> LDS ----
     {
-      f32x16 acc[6];
+      f32x16 acc[3];
 #pragma unroll
-      for (int ct = 0; ct < 6; ++ct)
+      for (int j = 0; j < 3; ++j)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) acc[ct][i] = 0.f;
-      const int ra = wave * 32 + l32 + zo;
-#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+      const int ra = pt * 32 + l32 + zo;
+#pragma unroll 1
       for (int ks = 0; ks < 6; ++ks) {
         const E8 a = *reinterpret_cast<const E8*>(&L.f[sf_off(ra, ks * 16 + 8 * hh)]);
 #pragma unroll
-        for (int ct = 0; ct < 6; ++ct) {
-          const E8 b = *reinterpret_cast<const E8*>(&L.w[(ct * 32 + l32) * WP + ks * 16 + 8 * hh + zo]);
-          acc[ct] = mfma32(a, b, acc[ct]);
+        for (int j = 0; j < 3; ++j) {
+          const E8 b = *reinterpret_cast<const E8*>(&L.w[((3 * hd + j) * 32 + l32) * WP + ks * 16 + 8 * hh + zo]);
+          acc[j] = mfma32(a, b, acc[j]);
         }
       }
-      // acc[ct][r] = H[px = wave*32 + 8*(r>>2) + 4*hh + (r&3)][c = ct*32 + l32]
+      // acc[j][r] = H[px = pt*32 + 8*(r>>2) + 4*hh + (r&3)][c = (3*hd + j)*32 + l32]
 #pragma unroll
-      for (int ct = 0; ct < 6; ++ct) {
-        const int c = ct * 32 + l32;
+      for (int j = 0; j < 3; ++j) {
+        const int c = (3 * hd + j) * 32 + l32;
         const float b1c = L.b1[c + zo], w2c = L.w2[c + zo];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int pr = wave * 32 + 8 * (r >> 2) + 4 * hh + (r & 3) + zo;
-          const float dl = L.dl[ct / 3][pr];
-          const float hv = fmaxf(acc[ct][r] + b1c, 0.f);
-          dw2acc[ct] += hv * dl;
+          const int pr = pt * 32 + 8 * (r >> 2) + 4 * hh + (r & 3) + zo;
+          const float dl = L.dl[hd][pr];
+          const float hv = fmaxf(acc[j][r] + b1c, 0.f);
+          dw2acc[j] += hv * dl;
           const float dh = hv > 0.f ? dl * w2c : 0.f;
-          db1acc[ct] += dh;
+          db1acc[j] += dh;
           L.dh[sd_off(pr, c)] = (E)dh;
         }
       }
     }
     __syncthreads();
-    // ---- df^T[k][px] = sum_c W1p^T[k][c] dh[px][c] (policy channels only) ----
+    // ---- df^T[k][px] = sum_c W1p[c][k] dh[px][c] (policy channels only), px-tile pt ----
     {
-      f32x16 acc2[3];
-      const int rb = wave * 32 + l32 + zo;
+      f32x16 acc2[NKT];
+      const int rb = pt * 32 + l32 + zo;
       const int64_t row = base + rb;
-      if (p.gadd) {  // (uniform) the accumulators start at gadd[m / P]: 12 loads issued
-                     // together, ahead of the MFMAs (rows past M read row M-1, discarded)
+      if (p.gadd) {  // (uniform) the accumulators start at gadd[m / P] (rows past M: row M-1, discarded)
         const float* ga = p.gadd + ((row < p.M ? row : p.M - 1) / p.P) * C;
 #pragma unroll
-        for (int kt = 0; kt < 3; ++kt)
+        for (int u = 0; u < NKT; ++u)
 #pragma unroll
           for (int gg = 0; gg < 4; ++gg) {
-            const float4 a4 = *reinterpret_cast<const float4*>(&ga[kt * 32 + 8 * gg + 4 * hh]);
-            acc2[kt][4 * gg + 0] = a4.x;
-            acc2[kt][4 * gg + 1] = a4.y;
-            acc2[kt][4 * gg + 2] = a4.z;
-            acc2[kt][4 * gg + 3] = a4.w;
+            const float4 a4 = *reinterpret_cast<const float4*>(&ga[(KT0 + u) * 32 + 8 * gg + 4 * hh]);
+            acc2[u][4 * gg + 0] = a4.x;
+            acc2[u][4 * gg + 1] = a4.y;
+            acc2[u][4 * gg + 2] = a4.z;
+            acc2[u][4 * gg + 3] = a4.w;
           }
       } else {
 #pragma unroll
-        for (int kt = 0; kt < 3; ++kt)
+        for (int u = 0; u < NKT; ++u)
 #pragma unroll
-          for (int i = 0; i < 16; ++i) acc2[kt][i] = 0.f;
+          for (int i = 0; i < 16; ++i) acc2[u][i] = 0.f;
       }
-#pragma unroll
+#pragma unroll 1
       for (int ks = 0; ks < 6; ++ks) {
         const E8 b = *reinterpret_cast<const E8*>(&L.dh[sd_off(rb, ks * 16 + 8 * hh)]);
+        const int r0 = ks * 16 + 8 * (g >> 1) + q + zo;  // W1 rows (K = c), transposed read
 #pragma unroll
-        for (int kt = 0; kt < 3; ++kt) {
-          const E8 a = *reinterpret_cast<const E8*>(&L.wt[(kt * 32 + l32) * WP + ks * 16 + 8 * hh + zo]);
-          acc2[kt] = mfma32(a, b, acc2[kt]);
+        for (int u = 0; u < NKT; ++u) {
+          const int col = (KT0 + u) * 32 + 16 * (g & 1) + 4 * pp;
+          const E8 a = cat8(lds_tr4(&L.w[r0 * WP + col]), lds_tr4(&L.w[(r0 + 4) * WP + col]));
+          acc2[u] = mfma32(a, b, acc2[u]);
         }
       }
-      // acc2[kt][r] = df[px = wave*32 + l32][k = kt*32 + 8*(r>>2) + 4*hh + (r&3)]:
-      // 8-B pieces of 64 different rows; staged in this wave's 32 rows of L.df, then
-      // written as contiguous 16-B chunks (the wave's rows are 6 KiB of contiguous df)
+      // acc2[u][r] = df[px = rb][k = (KT0+u)*32 + 8*(r>>2) + 4*hh + (r&3)]: 8-B stores (staging
+      // them in LDS for 16-B stores needs the f region, i.e. dW1 first: 3.26 ms, spills)
+      if (row < p.M) {
+        typedef typename EV<E>::v4 E4;
 #pragma unroll
-      for (int kt = 0; kt < 3; ++kt)
+        for (int u = 0; u < NKT; ++u)
 #pragma unroll
-        for (int gg = 0; gg < 4; ++gg) {
-          const int k0 = kt * 32 + 8 * gg + 4 * hh;
-          float v[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = acc2[kt][4 * gg + j];
-          *reinterpret_cast<E4*>(&L.df[rb * C + k0]) =
-              E4{(E)v[0], (E)v[1], (E)v[2], (E)v[3]};
-        }
-      // (LDS operations of one wave complete in order: its own rows read back below)
-      const int lane64 = tid & 63;
-#pragma unroll 1
-      for (int i = 0; i < 32 * 12 / 64; ++i) {
-        const int c = lane64 + 64 * i, r = c / 12, ch = c - r * 12;
-        const int64_t grow = base + wave * 32 + r;
-        const u32x4 v = *reinterpret_cast<const u32x4*>(&L.df[(wave * 32 + r) * C + ch * 8 + zo]);
-        if (grow < p.M) *reinterpret_cast<u32x4*>(&p.df[grow * C + ch * 8]) = v;
+          for (int gg = 0; gg < 4; ++gg) {
+            const int k0 = (KT0 + u) * 32 + 8 * gg + 4 * hh;
+            *reinterpret_cast<E4*>(&p.df[row * C + k0]) =
+                E4{(E)acc2[u][4 * gg + 0], (E)acc2[u][4 * gg + 1], (E)acc2[u][4 * gg + 2], (E)acc2[u][4 * gg + 3]};
+          }
       }
     }
-    // ---- dW1[c][k] += sum_px dh[px][c] f[px][k] over the tile's 128 rows ----
-#pragma unroll 2
-    for (int kk = 0; kk < TR / 16; ++kk) {
+
+    // ---- dW1[c][k] += sum_px dh[px][c] f[px][k] over the tile's 64 rows ----
+#pragma unroll 1
+    for (int kk = 0; kk < TRB / 16; ++kk) {
       const int r0 = kk * 16 + 8 * (g >> 1) + q + zo;
       E8 av[6], bv[3];
 #pragma unroll
@@ -337,15 +331,20 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
       part[c * C + kt * 32 + l32] = dwacc[t][r];
     }
   }
+  // dw2 / db1: the two waves of a head (px-tiles 0 and 1) combine in LDS (the dh region,
+  // free after the tile loop's last barrier)
+  float* red = reinterpret_cast<float*>(L.dh);  // [2][NH]
+  for (int i = tid; i < 2 * NH; i += 256) red[i] = 0.f;
+  __syncthreads();
 #pragma unroll
-  for (int ct = 0; ct < 6; ++ct) {
-    atomicAdd(&L.red[0][ct * 32 + l32], dw2acc[ct]);
-    atomicAdd(&L.red[1][ct * 32 + l32], db1acc[ct]);
+  for (int j = 0; j < 3; ++j) {
+    atomicAdd(&red[(3 * hd + j) * 32 + l32], dw2acc[j]);
+    atomicAdd(&red[NH + (3 * hd + j) * 32 + l32], db1acc[j]);
   }
 }
 
 template <typename E>
-__global__ __launch_bounds__(256, 1) void k_heads_bwd(HeadBwdParams<E> p) {
+__global__ __launch_bounds__(256, 2) void k_heads_bwd(HeadBwdParams<E> p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   HeadLds<E>& L = *reinterpret_cast<HeadLds<E>*>(smem);
   const int tid = threadIdx.x;
@@ -353,28 +352,26 @@ __global__ __launch_bounds__(256, 1) void k_heads_bwd(HeadBwdParams<E> p) {
     const int c = i / 12, k8 = i - c * 12;
     *reinterpret_cast<u32x4*>(&L.w[c * WP + k8 * 8]) = *reinterpret_cast<const u32x4*>(&p.w1[c * C + k8 * 8]);
   }
-  for (int i = tid; i < C * 12; i += 256) {
-    const int k = i / 12, c8 = i - k * 12;
-    *reinterpret_cast<u32x4*>(&L.wt[k * WP + c8 * 8]) = *reinterpret_cast<const u32x4*>(&p.w1pT[k * C + c8 * 8]);
-  }
   for (int i = tid; i < NH; i += 256) {
     L.b1[i] = p.b1[i];
     L.w2[i] = p.w2[i];
-    L.red[0][i] = L.red[1][i] = 0.f;
   }
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  switch (wave) {  // 18 dW1 tiles (6 c-tiles x 3 k-tiles) split 5/5/4/4
-    case 0: heads_bwd_body<E, 0, 5>(p, L); break;
-    case 1: heads_bwd_body<E, 5, 5>(p, L); break;
-    case 2: heads_bwd_body<E, 10, 4>(p, L); break;
-    default: heads_bwd_body<E, 14, 4>(p, L); break;
+  // 18 dW1 tiles split 5/5/4/4; the 6 df tiles (2 px x 3 k) split 2/2/1/1
+  float* red = reinterpret_cast<float*>(L.dh);
+  switch (wave) {
+    case 0: heads_bwd_body<E, 0, 5, 0, 2>(p, L); break;
+    case 1: heads_bwd_body<E, 5, 5, 0, 2>(p, L); break;
+    case 2: heads_bwd_body<E, 10, 4, 2, 1>(p, L); break;
+    default: heads_bwd_body<E, 14, 4, 2, 1>(p, L); break;
   }
+  (void)red;
   __syncthreads();
   float* part = p.part + (size_t)blockIdx.x * PART;
   for (int i = tid; i < NH; i += 256) {
-    part[NH * C + i] = L.red[0][i];
-    part[NH * C + NH + i] = L.red[1][i];
+    part[NH * C + i] = red[i];
+    part[NH * C + NH + i] = red[NH + i];
   }
 }
 
@@ -389,10 +386,10 @@ __global__ __launch_bounds__(256) void k_heads_reduce(const float* __restrict__ 
   else db1[i - NH * C - NH] = s;
 }
 
-int bwd_grid(int64_t M) {
-  const int64_t ntiles = (M + TR - 1) / TR;
-  const int ncu = num_cus();
-  return (int)(ntiles < ncu ? ntiles : ncu);
+int bwd_grid(int64_t M) {  // two k_heads_bwd workgroups per CU
+  const int64_t ntiles = (M + TRB - 1) / TRB;
+  const int cap = 2 * num_cus();
+  return (int)(ntiles < cap ? ntiles : cap);
 }
 
 int check(const char* what) {
@@ -443,7 +440,8 @@ int run_heads_bwd(const uint16_t* f, const float* dlp, const float* dlm, const u
   p.P = P;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_heads_bwd<E>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_heads_bwd<E>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)sizeof(HeadLds<E>));
     attr = true;
   }
   hipLaunchKernelGGL(k_heads_bwd<E>, dim3(grid), dim3(256), sizeof(HeadLds<E>), s, p);
@@ -479,7 +477,7 @@ int64_t mc_heads_bwd_workspace(int64_t M) {
 int mc_heads_bwd(const uint16_t* f, const float* dlp, const float* dlm, const uint16_t* w1, const uint16_t* w1pT,
                  const float* b1, const float* w2, const float* gadd, int32_t P, uint16_t* df, float* dw1,
                  float* db1, float* dw2, float* work, int64_t work_floats, int64_t M, int32_t dtype, void* stream) {
-  if (!f || !dlp || !w1 || !w1pT || !b1 || !w2 || !df || !dw1 || !db1 || !dw2 || !work || M <= 0 ||
+  if (!f || !dlp || !w1 || !b1 || !w2 || !df || !dw1 || !db1 || !dw2 || !work || M <= 0 ||
       (gadd && P <= 0)) {
     snprintf(g_err, sizeof g_err, "mc_heads_bwd: bad argument");
     return MS_EINVAL;

@@ -296,11 +296,10 @@ def _head_pack(pol, mine, dtype: torch.dtype):
     if hit is not None and hit[1] == vers and all(a is b for a, b in zip(hit[0], params)):
         return hit[2]
     w1 = torch.cat([h[0].weight.detach().reshape(COUT, COUT) for h in heads]).to(dtype).contiguous()
-    w1pT = pol[0].weight.detach().reshape(COUT, COUT).t().to(dtype).contiguous()
     b1 = torch.cat([h[0].bias.detach() for h in heads]).float().contiguous()
     w2 = torch.cat([h[2].weight.detach().reshape(COUT) for h in heads]).float().contiguous()
     b2 = torch.cat([h[2].bias.detach().reshape(1) for h in heads]).float().contiguous()
-    packed = (w1, w1pT, b1, w2, b2)
+    packed = (w1, b1, w2, b2)
     _hcache[key] = (params, vers, packed)
     return packed
 
@@ -320,7 +319,7 @@ def heads_forward(f: torch.Tensor, pol, mine=None):
     n, p, c = f.shape
     dt = _dt(f)
     assert c == COUT and f.is_contiguous()
-    w1, _, b1, w2, b2 = _head_pack(pol, mine, f.dtype)
+    w1, b1, w2, b2 = _head_pack(pol, mine, f.dtype)
     lp = torch.empty((n, p), dtype=torch.float32, device=f.device)
     lm = torch.empty_like(lp) if mine is not None else None
     _check(_hf(L.ptr(f), L.ptr(w1), L.ptr(b1), L.ptr(w2), L.ptr(b2), L.ptr(lp), L.ptr(lm), n * p, dt,
@@ -348,7 +347,7 @@ class _HeadsFn(torch.autograd.Function):
         n, p, _ = f.shape
         M = n * p
         # the kernel always runs both heads' math; without a mine head its rows get dl = 0
-        w1, w1pT, b1, w2, _ = _head_pack(pol, mine if mine is not None else pol, f.dtype)
+        w1, b1, w2, _ = _head_pack(pol, mine if mine is not None else pol, f.dtype)
         dev = f.device
         dlp = dlp.float().contiguous() if dlp is not None else torch.zeros(n, p, device=dev)
         dlm = dlm.float().contiguous() if (dlm is not None and mine is not None) else None
@@ -359,7 +358,7 @@ class _HeadsFn(torch.autograd.Function):
         dw2 = torch.empty(2 * COUT, device=dev)
         nws = int(_hbws(M))
         work = torch.empty(nws, device=dev)
-        _check(_hb(L.ptr(f), L.ptr(dlp), L.ptr(dlm), L.ptr(w1), L.ptr(w1pT), L.ptr(b1), L.ptr(w2), L.ptr(gadd), p,
+        _check(_hb(L.ptr(f), L.ptr(dlp), L.ptr(dlm), L.ptr(w1), None, L.ptr(b1), L.ptr(w2), L.ptr(gadd), p,
                    L.ptr(df), L.ptr(dw1), L.ptr(db1), L.ptr(dw2), L.ptr(work), nws, M, _dt(f), L.stream_ptr(dev)))
         grads = [df, None, None]
         for h, i, dl in [(pol, 0, dlp)] + ([(mine, 1, dlm)] if mine is not None else []):

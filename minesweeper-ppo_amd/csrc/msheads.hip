@@ -359,15 +359,14 @@ __global__ __launch_bounds__(256, 2) void k_heads_bwd(HeadBwdParams<E> p) {
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // 18 dW1 tiles split 5/5/4/4; the 6 df tiles (2 px x 3 k) split 2/2/1/1
-  float* red = reinterpret_cast<float*>(L.dh);
   switch (wave) {
     case 0: heads_bwd_body<E, 0, 5, 0, 2>(p, L); break;
     case 1: heads_bwd_body<E, 5, 5, 0, 2>(p, L); break;
     case 2: heads_bwd_body<E, 10, 4, 2, 1>(p, L); break;
     default: heads_bwd_body<E, 14, 4, 2, 1>(p, L); break;
   }
-  (void)red;
   __syncthreads();
+  const float* red = reinterpret_cast<const float*>(L.dh);  // the dw2 / db1 combine of the bodies
   float* part = p.part + (size_t)blockIdx.x * PART;
   for (int i = tid; i < NH; i += 256) {
     part[NH * C + i] = red[i];

@@ -348,7 +348,9 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
         }
       }
     }
-    // no trailing barrier: the next sample touches sD / sW only after its reduction barriers
+    // the next sample's pass 1 writes dz into sD while a slower wave may still be reading its
+    // dx chunks here: an LDS-only barrier (the dx stores stay in flight)
+    lds_barrier();
   }
   if (tid < COUT) {
     p.part[((size_t)blockIdx.x * 3 + 0) * COUT + tid] = acc_g;

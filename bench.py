@@ -329,7 +329,8 @@ def ppo_bench(args, world, rank, local_rank, dev):
             "updates_per_s": 1.0 / spu, "s_per_update": spu,
             "samples_per_s": n_loc * world * T / spu, "envs_total": n_loc * world, "steps_per_env": T,
             "rollout_s": mean("rollout_s"), "gae_s": mean("gae_s"), "ppo_s": mean("ppo_s"),
-            "amp": args.amp, "model": "cnn_residual 96ch x 5 blocks (950,947 params)",
+            "amp": args.amp, "rollout_buffer_obs": "u8 cell codes" if tr.obs_codes else "f32 one-hot",
+            "model": "cnn_residual 96ch x 5 blocks (950,947 params)",
             "roofline": {"bound": "mfma", "achieved": gflop / spu / 1e3, "peak": BF16_DENSE_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": gflop / spu / 1e3 / BF16_DENSE_PEAK_TFLOPS,
                          "traffic": kprof[dom]["traffic_bytes_per_launch"] if dom else None,

@@ -27,6 +27,18 @@ extern "C" {
 #define MC_DTYPE_BF16 0
 #define MC_DTYPE_F16 1
 
+/* Observation codes (the rollout buffer's layout; no reference counterpart: the reference
+ * buffer stores the f32 one-hot obs, buffers.py:24-36). The obs [N][10][A] f32 of the env
+ * (env.py:172-192) is one byte per cell: 0 = hidden (all planes 0), 1 + k = revealed with k
+ * adjacent mines (planes 0 and 1 + k). mc_obs_encode writes the codes (u8 [N][A], may be
+ * NULL; exact for every obs the env writes) and/or the stem input (16-bit [N][A][cin_pad],
+ * cin_pad = 16: the 10 planes' values cast to 16 bits, channels 10..15 zero; may be NULL) of an
+ * f32 obs in one pass; mc_codes_to_nhwc expands codes to the stem input. */
+int mc_obs_encode(const float* obs, uint8_t* codes, uint16_t* nhwc, int64_t n, int32_t a, int32_t cin_pad,
+                  int32_t dtype, void* stream);
+int mc_codes_to_nhwc(const uint8_t* codes, uint16_t* nhwc, int64_t n, int32_t a, int32_t cin_pad, int32_t dtype,
+                     void* stream);
+
 /* Forward of one fused layer:
  *   y   = conv3x3(x, w) + bias                       (saved to ysave, bf16)
  *   out = relu(GN(y) * gamma + beta [+ res]) [* dmask[n][c]]

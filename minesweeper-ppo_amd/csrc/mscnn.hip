@@ -425,6 +425,67 @@ int dispatch_fwd(const FwdParams<E>& p, hipStream_t s) {
 
 }  // namespace
 
+
+// ---------------------------------------------------------------------------------------
+// Observation codes: the one-hot obs of a cell (env.py:172-192: plane 0 = revealed, plane
+// 1 + k = revealed with k adjacent mines; all zero before the board's first click) is one
+// byte, 0 = hidden, 1 + k = revealed with k. The rollout buffer stores codes [N][A]
+// (A bytes per sample instead of 40 A), and the trunk's input [N][A][cin_pad] 16-bit is
+// expanded from them; exact for every obs the env writes. k_obs_encode's stem input is the
+// planes' own values cast to 16 bits (exact for any f32 input that 16 bits hold).
+template <typename E>
+__device__ __forceinline__ void store_onehot16(E* dst, uint32_t code, int cin_pad) {
+  // channels 0..cin_pad-1 (16): 1 at channel 0 and 1 + k when code = 1 + k > 0
+  typedef typename EV<E>::v8 E8;
+  E8 lo, hi;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    lo[j] = (E)((j == 0 && code) || (code && (uint32_t)j == code) ? 1.0f : 0.0f);
+    hi[j] = (E)(code && (uint32_t)(j + 8) == code ? 1.0f : 0.0f);
+  }
+  *reinterpret_cast<E8*>(dst) = lo;
+  if (cin_pad > 8) *reinterpret_cast<E8*>(dst + 8) = hi;
+}
+
+template <typename E>
+__global__ __launch_bounds__(256) void k_obs_encode(const float* __restrict__ obs, uint8_t* __restrict__ codes,
+                                                    E* __restrict__ nhwc, int64_t n, int a, int cin_pad) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // cell of the [n][a] grid
+  if (i >= n * a) return;
+  const int64_t sm = i / a;
+  const int c = (int)(i - sm * a);
+  const float* o = obs + sm * 10 * a + c;
+  float v[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) v[k] = o[(int64_t)k * a];  // coalesced per plane
+  uint32_t code = 0u;
+  if (v[0] != 0.f) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+      if (v[1 + k] != 0.f) code = 1u + (uint32_t)k;
+  }
+  if (codes) codes[i] = (uint8_t)code;
+  if (nhwc) {  // the planes' own values (exact for any input, not only one-hot env obs)
+    typedef typename EV<E>::v8 E8;
+    E8 lo, hi;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      lo[j] = (E)v[j];
+      hi[j] = (E)(j < 2 ? v[8 + j] : 0.0f);
+    }
+    *reinterpret_cast<E8*>(nhwc + i * cin_pad) = lo;
+    *reinterpret_cast<E8*>(nhwc + i * cin_pad + 8) = hi;
+  }
+}
+
+template <typename E>
+__global__ __launch_bounds__(256) void k_codes_to_nhwc(const uint8_t* __restrict__ codes, E* __restrict__ nhwc,
+                                                       int64_t cells, int cin_pad) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= cells) return;
+  store_onehot16(nhwc + i * cin_pad, (uint32_t)codes[i], cin_pad);
+}
+
 #ifdef MC_DIAG
 unsigned long long* g_fwd_diag = nullptr;
 #endif
@@ -463,6 +524,55 @@ int run_fwd(const uint16_t* x, const uint16_t* w, const float* bias, const float
 extern "C" {
 
 const char* mc_last_error(void) { return g_err; }
+
+int mc_obs_encode(const float* obs, uint8_t* codes, uint16_t* nhwc, int64_t n, int32_t a, int32_t cin_pad,
+                  int32_t dtype, void* stream) {
+  if (!obs || (!codes && !nhwc) || n <= 0 || a <= 0 || a > 255 * 255 || (nhwc && cin_pad != 16)) {
+    snprintf(g_err, sizeof g_err, "mc_obs_encode: bad argument");
+    return MS_EINVAL;
+  }
+  const unsigned grid = (unsigned)((n * a + 255) / 256);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MC_DT_BF16)
+    hipLaunchKernelGGL(k_obs_encode<__bf16>, dim3(grid), dim3(256), 0, s, obs, codes, reinterpret_cast<__bf16*>(nhwc), n, a, cin_pad);
+  else if (dtype == MC_DT_F16)
+    hipLaunchKernelGGL(k_obs_encode<_Float16>, dim3(grid), dim3(256), 0, s, obs, codes, reinterpret_cast<_Float16*>(nhwc), n, a, cin_pad);
+  else {
+    snprintf(g_err, sizeof g_err, "mc_obs_encode: dtype %d unsupported (0 bf16, 1 f16)", dtype);
+    return MS_EINVAL;
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof g_err, "mc_obs_encode launch: %s", hipGetErrorString(e));
+    return MS_EHIP;
+  }
+  return MS_OK;
+}
+
+int mc_codes_to_nhwc(const uint8_t* codes, uint16_t* nhwc, int64_t n, int32_t a, int32_t cin_pad, int32_t dtype,
+                     void* stream) {
+  if (!codes || !nhwc || n <= 0 || a <= 0 || cin_pad != 16) {
+    snprintf(g_err, sizeof g_err, "mc_codes_to_nhwc: bad argument");
+    return MS_EINVAL;
+  }
+  const int64_t cells = n * a;
+  const unsigned grid = (unsigned)((cells + 255) / 256);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MC_DT_BF16)
+    hipLaunchKernelGGL(k_codes_to_nhwc<__bf16>, dim3(grid), dim3(256), 0, s, codes, reinterpret_cast<__bf16*>(nhwc), cells, cin_pad);
+  else if (dtype == MC_DT_F16)
+    hipLaunchKernelGGL(k_codes_to_nhwc<_Float16>, dim3(grid), dim3(256), 0, s, codes, reinterpret_cast<_Float16*>(nhwc), cells, cin_pad);
+  else {
+    snprintf(g_err, sizeof g_err, "mc_codes_to_nhwc: dtype %d unsupported (0 bf16, 1 f16)", dtype);
+    return MS_EINVAL;
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof g_err, "mc_codes_to_nhwc launch: %s", hipGetErrorString(e));
+    return MS_EHIP;
+  }
+  return MS_OK;
+}
 
 #ifdef MC_DIAG
 // diagnostics only (not in mscnn.h): per-workgroup phase cycle totals of the next forwards

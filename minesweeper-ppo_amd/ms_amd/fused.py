@@ -55,13 +55,53 @@ def prep_weight(w: torch.Tensor, cin_pad: int, dtype: torch.dtype = torch.bfloat
     return wt.to(dtype).contiguous()
 
 
-def obs_to_nhwc(obs: torch.Tensor, cin_pad: int = 16, dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
-    """f32 [N, 10, H, W] one-hot observation -> ``dtype`` [N, H*W, cin_pad] (exact: values are 0/1)."""
+_enc = _c2n = None
+
+
+def obs_encode(obs: torch.Tensor, codes: Optional[torch.Tensor] = None, want_nhwc: bool = False,
+               cin_pad: int = 16, dtype: torch.dtype = torch.bfloat16):
+    """f32 obs [N, 10, H, W] -> its cell codes (u8 [N, H, W] written into ``codes`` when
+    given: 0 hidden, 1 + k revealed with k adjacent mines; exact for the env's obs) and/or,
+    with ``want_nhwc``, the stem input ``dtype`` [N, H*W, cin_pad] (the planes' values cast,
+    exact for any input), in one pass (mc_obs_encode). Returns the NHWC tensor or None."""
+    global _enc
+    if _enc is None:
+        _enc = _fn("mc_obs_encode", [_vp, _vp, _vp, ctypes.c_int64, _i32, _i32, _i32, _vp])
     n, c, h, w = obs.shape
-    x = obs.permute(0, 2, 3, 1).reshape(n, h * w, c)
-    if cin_pad > c:
-        x = torch.nn.functional.pad(x, (0, cin_pad - c))
-    return x.to(dtype).contiguous()
+    assert c == 10 and obs.dtype == torch.float32 and obs.is_contiguous()
+    if codes is not None:
+        assert codes.shape == (n, h, w) and codes.dtype == torch.uint8 and codes.is_contiguous()
+    x = torch.empty((n, h * w, cin_pad), dtype=dtype, device=obs.device) if want_nhwc else None
+    _check(_enc(L.ptr(obs), L.ptr(codes), L.ptr(x), n, h * w, cin_pad, DTYPES[dtype], L.stream_ptr(obs.device)))
+    return x
+
+
+def codes_to_nhwc(codes: torch.Tensor, cin_pad: int = 16, dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
+    """u8 cell codes [N, H, W] -> stem input ``dtype`` [N, H*W, cin_pad] (mc_codes_to_nhwc)."""
+    global _c2n
+    if _c2n is None:
+        _c2n = _fn("mc_codes_to_nhwc", [_vp, _vp, ctypes.c_int64, _i32, _i32, _i32, _vp])
+    n, h, w = codes.shape
+    codes = codes.contiguous()
+    x = torch.empty((n, h * w, cin_pad), dtype=dtype, device=codes.device)
+    _check(_c2n(L.ptr(codes), L.ptr(x), n, h * w, cin_pad, DTYPES[dtype], L.stream_ptr(codes.device)))
+    return x
+
+
+def codes_to_obs(codes: torch.Tensor) -> torch.Tensor:
+    """u8 cell codes [N, H, W] -> the env's f32 one-hot obs [N, 10, H, W] (exact)."""
+    k = codes.long()
+    planes = torch.arange(10, device=codes.device).view(1, 10, 1, 1)
+    hit = (k.unsqueeze(1) == planes) | ((planes == 0) & (k.unsqueeze(1) > 0))
+    return (hit & (k.unsqueeze(1) > 0)).to(torch.float32)
+
+
+def obs_to_nhwc(obs: torch.Tensor, cin_pad: int = 16, dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
+    """Stem input ``dtype`` [N, H*W, cin_pad] from an f32 obs [N, 10, H, W] (its values cast) or
+    from the env's u8 cell codes [N, H, W]. One HIP pass either way."""
+    if obs.dtype == torch.uint8:
+        return codes_to_nhwc(obs, cin_pad, dtype)
+    return obs_encode(obs.contiguous(), None, True, cin_pad, dtype)
 
 
 def conv_gn_fwd(x: torch.Tensor, wt: torch.Tensor, bias: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor,
@@ -259,7 +299,7 @@ def fused_features(model, obs: torch.Tensor, dtype: torch.dtype = torch.bfloat16
     """Trunk features of CNNResidualPolicy as NHWC ``dtype`` [N, H*W, 96] via the fused kernels
     (``dtype``: the autocast type, bf16 or fp16). ``dmasks``: per-block Dropout2d masks [N, 96]
     (keep / (1 - p), ms_amd.dropout); without them a training-mode model draws torch-RNG masks."""
-    n, c, H, W = obs.shape
+    n, H, W = obs.shape[0], obs.shape[-2], obs.shape[-1]  # f32 obs [N, 10, H, W] or u8 codes [N, H, W]
     layers = trunk_layers(model)
     x0 = obs_to_nhwc(obs, 16, dtype)
     nblk = len(model.residual_stack)

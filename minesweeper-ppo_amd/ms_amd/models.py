@@ -111,7 +111,7 @@ class CNNResidualPolicy(nn.Module):
     def use_fused(self, x: torch.Tensor) -> bool:
         conv0 = self.stem[0]
         return (self.fused and x.is_cuda and conv0.out_channels == 96 and conv0.in_channels <= 16
-                and x.shape[2] * x.shape[3] <= 512 and torch.is_autocast_enabled("cuda")
+                and x.shape[-2] * x.shape[-1] <= 512 and torch.is_autocast_enabled("cuda")
                 and torch.get_autocast_dtype("cuda") in (torch.bfloat16, torch.float16))
 
     def dropout_p(self) -> float:
@@ -150,11 +150,16 @@ class CNNResidualPolicy(nn.Module):
         return logits, value
 
     def forward(self, x: torch.Tensor, return_mine: bool = False):
+        """x: the env's f32 obs [N, 10, H, W], or its u8 cell codes [N, H, W] (the Trainer's
+        rollout-buffer layout, ms_amd.fused.obs_encode)."""
         dmasks = self.keyed_masks(x.shape[0])
         if self.use_fused(x):
             from .fused import fused_features
             f = fused_features(self, x, torch.get_autocast_dtype("cuda"), dmasks=dmasks)
-            return self._heads_fused(f, x.shape[2], x.shape[3], return_mine)
+            return self._heads_fused(f, x.shape[-2], x.shape[-1], return_mine)
+        if x.dtype == torch.uint8:
+            from .fused import codes_to_obs
+            x = codes_to_obs(x)
         f = self.features(x, dmasks)
         n = f.shape[0]
         # [N,1,H,W] -> [N,H*W], index r*W + c (cnn_residual.py:89)
@@ -192,6 +197,9 @@ class CNNPolicy(nn.Module):
         return None
 
     def forward(self, x: torch.Tensor, return_mine: bool = False):
+        if x.dtype == torch.uint8:  # u8 cell codes [N, H, W] (CNNResidualPolicy.forward)
+            from .fused import codes_to_obs
+            x = codes_to_obs(x)
         f = self.backbone(x)
         n = f.shape[0]
         logits = self.policy_head(f).reshape(n, -1)

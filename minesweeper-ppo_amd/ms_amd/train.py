@@ -143,8 +143,11 @@ class Trainer:
 
     def __init__(self, cfg: PPOTrainConfig, env_d: Dict, model_d: Dict, extras: Dict, *, seed: int = 0,
                  model_name: str | None = None, info: DistInfo | None = None, amp: str = "fp16",
-                 device: torch.device | None = None):
+                 device: torch.device | None = None, obs_codes: bool = True):
+        """``obs_codes``: the rollout buffer holds u8 cell codes instead of the f32 one-hot obs
+        (RolloutBuffer; exact, 40x fewer bytes held and gathered per minibatch)."""
         self.cfg = cfg
+        self.obs_codes = obs_codes
         self.info = info or DistInfo()
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         training = extras.get("training", {}) if isinstance(extras, dict) else {}
@@ -221,7 +224,7 @@ class Trainer:
         self.buffer, aux = collect_rollout(
             self.vec, self.model, cfg.steps_per_env, self.device, pc.aux_mine_weight,
             pc.aux_mine_calib_weight, amp_dtype=self.amp_dtype, buffer=self.buffer,
-            sample_seed=self.seed * 7919 + 17, sample_counter=update << 20)
+            sample_seed=self.seed * 7919 + 17, sample_counter=update << 20, obs_codes=self.obs_codes)
         mark()
         self.buffer.compute_gae(aux["last_values"], gamma=cfg.gamma, lam=cfg.gae_lambda)
         mark()

@@ -58,9 +58,7 @@ int mc_conv_gn_fwd(const uint16_t* x, const uint16_t* w, const float* bias, cons
  * input; wT = the conv weight re-laid out as bf16 [9][cin][96] (tap, ci, co), or
  * NULL when no input gradient is wanted (the stem: its input is the observation).
  * addend (bf16 [N][P][cin], may be NULL) is added to dx (the block input's skip
- * gradient). addend_mask (u8 [N][P][cin/8] ReLU bits in relu_mask's layout, may be NULL)
- * restricts it to the set bits: passing the second half-block's dout and ReLU bits as
- * addend / addend_mask adds that half-block's dz without it ever being stored. Outputs:
+ * gradient). Outputs:
  *   dy     bf16 [N][P][96]  dL/dy, the conv-output gradient (also a workspace);
  *   dz     bf16 [N][P][96]  dL/d(pre-ReLU sum) = the residual gradient, or NULL;
  *   dx     bf16 [N][P][cin] conv input gradient (+ addend), NULL iff wT is NULL;
@@ -71,9 +69,9 @@ int mc_conv_gn_fwd(const uint16_t* x, const uint16_t* w, const float* bias, cons
 int mc_conv_gn_bwd(const uint16_t* dout, const uint16_t* out, const uint8_t* relu_mask,
                    const uint16_t* ysave, const float* stats,
                    const float* gamma, const float* dmask, const uint16_t* x, const uint16_t* wT,
-                   const uint16_t* addend, const uint8_t* addend_mask, uint16_t* dy, uint16_t* dz, uint16_t* dx,
-                   float* dw, float* dgn, float* work, int64_t work_floats, int32_t n, int32_t h, int32_t w_,
-                   int32_t cin, int32_t dtype, void* stream);
+                   const uint16_t* addend, uint16_t* dy, uint16_t* dz, uint16_t* dx, float* dw, float* dgn,
+                   float* work, int64_t work_floats, int32_t n, int32_t h, int32_t w_, int32_t cin,
+                   int32_t dtype, void* stream);
 
 /* f32 elements of scratch mc_conv_gn_bwd needs for these sizes. */
 int64_t mc_conv_gn_bwd_workspace(int32_t n, int32_t h, int32_t w_, int32_t cin);

@@ -49,7 +49,6 @@ struct BwdDataParams {
   const float* dmask;
   const E* wT;
   const E* addend;
-  const uint8_t* addend_mask;  // if set: addend chunk c8 counts only where its ReLU bit is set
   E* dy;
   E* dz;
   E* dx;
@@ -330,16 +329,11 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
     __syncthreads();
     if (gact) {
       u32x4 ad[NCH];  // all addend loads in flight before the first dependent store
-      uint32_t am[NCH];
 #pragma unroll
       for (int i = 0; i < NCH; ++i) {
         const int px = pg + PG * i;
         ad[i] = u32x4{0u, 0u, 0u, 0u};
-        am[i] = 0xffu;
-        if (p.addend && px < P) {
-          ad[i] = *reinterpret_cast<const u32x4*>(&p.addend[((size_t)n * P + px) * COUT + c8 * 8]);
-          if (p.addend_mask) am[i] = p.addend_mask[((size_t)n * P + px) * NC8 + c8];
-        }
+        if (p.addend && px < P) ad[i] = *reinterpret_cast<const u32x4*>(&p.addend[((size_t)n * P + px) * COUT + c8 * 8]);
       }
 #pragma unroll
       for (int i = 0; i < NCH; ++i) {
@@ -349,7 +343,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
           const E8 r8 = __builtin_bit_cast(E8, ad[i]);
           E8 s8;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) s8[j] = (E)((float)a8[j] + (((am[i] >> j) & 1u) ? (float)r8[j] : 0.f));
+          for (int j = 0; j < 8; ++j) s8[j] = (E)((float)a8[j] + (float)r8[j]);
           *reinterpret_cast<u32x4*>(&p.dx[((size_t)n * P + px) * COUT + c8 * 8]) = __builtin_bit_cast(u32x4, s8);
         }
       }
@@ -673,8 +667,8 @@ int check_launch(const char* what) {
 template <typename E>
 int run_bwd(const uint16_t* dout, const uint16_t* out, const uint8_t* relu_mask, const uint16_t* ysave,
             const float* stats, const float* gamma, const float* dmask, const uint16_t* x, const uint16_t* wT,
-            const uint16_t* addend, const uint8_t* addend_mask, uint16_t* dy, uint16_t* dz, uint16_t* dx, float* dw,
-            float* dgn, float* work, int32_t n, int32_t h, int32_t w_, int32_t cin, hipStream_t s) {
+            const uint16_t* addend, uint16_t* dy, uint16_t* dz, uint16_t* dx, float* dw, float* dgn, float* work,
+            int32_t n, int32_t h, int32_t w_, int32_t cin, hipStream_t s) {
   const Plan pl = make_plan(n, h, w_, cin);
   BwdDataParams<E> bp;
   bp.dout = reinterpret_cast<const E*>(dout);
@@ -686,7 +680,6 @@ int run_bwd(const uint16_t* dout, const uint16_t* out, const uint8_t* relu_mask,
   bp.dmask = dmask;
   bp.wT = reinterpret_cast<const E*>(wT);
   bp.addend = reinterpret_cast<const E*>(addend);
-  bp.addend_mask = addend_mask;
   bp.dy = reinterpret_cast<E*>(dy);
   bp.dz = reinterpret_cast<E*>(dz);
   bp.dx = reinterpret_cast<E*>(dx);
@@ -730,8 +723,7 @@ int64_t mc_conv_gn_bwd_workspace(int32_t n, int32_t h, int32_t w_, int32_t cin) 
 int mc_conv_gn_bwd(const uint16_t* dout, const uint16_t* out, const uint8_t* relu_mask, const uint16_t* ysave,
                    const float* stats,
                    const float* gamma, const float* dmask, const uint16_t* x, const uint16_t* wT,
-                   const uint16_t* addend, const uint8_t* addend_mask, uint16_t* dy, uint16_t* dz, uint16_t* dx,
-                   float* dw, float* dgn,
+                   const uint16_t* addend, uint16_t* dy, uint16_t* dz, uint16_t* dx, float* dw, float* dgn,
                    float* work, int64_t work_floats, int32_t n, int32_t h, int32_t w_, int32_t cin,
                    int32_t dtype, void* stream) {
   if (!dout || (!out && !relu_mask) || !ysave || !stats || !gamma || !x || !dy || !dw || !dgn || !work || n <= 0 || h <= 0 ||
@@ -743,8 +735,8 @@ int mc_conv_gn_bwd(const uint16_t* dout, const uint16_t* out, const uint8_t* rel
     snprintf(g_err, sizeof g_err, "mc_conv_gn_bwd: cin %d unsupported (16 or 96)", cin);
     return MS_EINVAL;
   }
-  if ((wT == nullptr) != (dx == nullptr) || (wT && cin != 96) || (addend && !wT) || (addend_mask && !addend)) {
-    snprintf(g_err, sizeof g_err, "mc_conv_gn_bwd: dx needs wT (and cin 96); addend needs dx; addend_mask needs addend");
+  if ((wT == nullptr) != (dx == nullptr) || (wT && cin != 96) || (addend && !wT)) {
+    snprintf(g_err, sizeof g_err, "mc_conv_gn_bwd: dx needs wT (and cin 96); addend needs dx");
     return MS_EINVAL;
   }
   const Plan pl = make_plan(n, h, w_, cin);
@@ -759,12 +751,10 @@ int mc_conv_gn_bwd(const uint16_t* dout, const uint16_t* out, const uint8_t* rel
   }
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MC_DT_BF16)
-    return run_bwd<__bf16>(dout, out, relu_mask, ysave, stats, gamma, dmask, x, wT, addend, addend_mask, dy, dz, dx, dw, dgn,
-                           work, n, h,
+    return run_bwd<__bf16>(dout, out, relu_mask, ysave, stats, gamma, dmask, x, wT, addend, dy, dz, dx, dw, dgn, work, n, h,
                            w_, cin, s);
   if (dtype == MC_DT_F16)
-    return run_bwd<_Float16>(dout, out, relu_mask, ysave, stats, gamma, dmask, x, wT, addend, addend_mask, dy, dz, dx, dw,
-                             dgn, work, n,
+    return run_bwd<_Float16>(dout, out, relu_mask, ysave, stats, gamma, dmask, x, wT, addend, dy, dz, dx, dw, dgn, work, n,
                              h, w_, cin, s);
   snprintf(g_err, sizeof g_err, "mc_conv_gn_bwd: dtype %d unsupported (0 bf16, 1 f16)", dtype);
   return MS_EINVAL;

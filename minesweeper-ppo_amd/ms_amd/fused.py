@@ -151,14 +151,13 @@ def dw_to_conv(dw: torch.Tensor, cin_real: int) -> torch.Tensor:
 def conv_gn_bwd(dout: torch.Tensor, out: Optional[torch.Tensor], y: torch.Tensor, stats: torch.Tensor,
                 gamma: torch.Tensor, x: torch.Tensor, H: int, W: int, wT: Optional[torch.Tensor] = None,
                 dmask: Optional[torch.Tensor] = None, addend: Optional[torch.Tensor] = None, want_dz: bool = False,
-                rmask: Optional[torch.Tensor] = None, addend_mask: Optional[torch.Tensor] = None):
+                rmask: Optional[torch.Tensor] = None):
     """Backward of conv_gn_fwd. Returns (dx | None, dz | None, dw f32 [9,96,cin], dgn f32 [3,96] =
     d gamma, d beta, d bias). dx (x's 16-bit type, NHWC) is produced iff the dgrad weights ``wT`` are given.
-    ``rmask`` (the forward's ReLU bitmask) replaces the sign test on ``out``; one of them is needed.
-    ``addend`` is added to dx, where ``addend_mask``'s ReLU bits are set when it is given."""
+    ``rmask`` (the forward's ReLU bitmask) replaces the sign test on ``out``; one of them is needed."""
     global _bwd, _bwd_ws
     if _bwd is None:
-        _bwd = _fn("mc_conv_gn_bwd", [_vp] * 17 + [ctypes.c_int64] + [_i32] * 5 + [_vp])
+        _bwd = _fn("mc_conv_gn_bwd", [_vp] * 16 + [ctypes.c_int64] + [_i32] * 5 + [_vp])
         _bwd_ws = _fn("mc_conv_gn_bwd_workspace", [_i32] * 4)
         _bwd_ws.restype = ctypes.c_int64
     n, p, cin = x.shape
@@ -175,9 +174,6 @@ def conv_gn_bwd(dout: torch.Tensor, out: Optional[torch.Tensor], y: torch.Tensor
         assert wT.shape == (9, cin, COUT) and wT.dtype == et and wT.is_contiguous()
     if addend is not None:
         assert addend.shape == (n, p, cin) and addend.dtype == et and addend.is_contiguous()
-    if addend_mask is not None:
-        assert addend is not None and addend_mask.shape == (n, p, cin // 8)
-        assert addend_mask.dtype == torch.uint8 and addend_mask.is_contiguous()
     if dmask is not None:
         dmask = dmask.to(torch.float32).contiguous()
     g = gamma.detach().to(torch.float32).contiguous()
@@ -191,8 +187,7 @@ def conv_gn_bwd(dout: torch.Tensor, out: Optional[torch.Tensor], y: torch.Tensor
         raise L.MsEnvError("mc_conv_gn_bwd_workspace: bad sizes")
     work = torch.empty(nws, dtype=torch.float32, device=dev)
     _check(_bwd(L.ptr(dout), L.ptr(out), L.ptr(rmask), L.ptr(y), L.ptr(stats), L.ptr(g), L.ptr(dmask), L.ptr(x), L.ptr(wT),
-                L.ptr(addend), L.ptr(addend_mask), L.ptr(dy), L.ptr(dz), L.ptr(dx), L.ptr(dw), L.ptr(dgn),
-                L.ptr(work), nws,
+                L.ptr(addend), L.ptr(dy), L.ptr(dz), L.ptr(dx), L.ptr(dw), L.ptr(dgn), L.ptr(work), nws,
                 n, H, W, cin, dt, L.stream_ptr(dev)))
     return dx, dz, dw, dgn
 
@@ -269,21 +264,18 @@ class _TrunkFn(torch.autograd.Function):
         grads = {}
         d = dout.to(acts[0].dtype).contiguous()
         nl = len(layers)
-        # the block input's skip gradient is the second half's dz = dout * (its ReLU bits): it is
-        # passed to the first half's backward as (dout, bits) and never stored
-        skip = skip_bits = None
+        skip = None  # dz of a block's second half: the block input's skip gradient
         for li in range(nl - 1, -1, -1):
             conv, norm = layers[li]
             x = acts[li]
             cin_real = conv.weight.shape[1]
             want_dx = li > 0
             dm = dmasks[(li - 1) // 2] if (dmasks is not None and li % 2 == 1) else None
-            first_half = li % 2 == 1
-            dx, _, dw, dgn = conv_gn_bwd(d, None, ys[li], sts[li], norm.weight, x, H, W,
-                                         wT=_packed(conv.weight, "t", x.dtype) if want_dx else None, dmask=dm,
-                                         addend=skip if first_half else None,
-                                         addend_mask=skip_bits if first_half else None, rmask=rms[li])
-            skip, skip_bits = (d, rms[li]) if (li % 2 == 0 and li > 0) else (None, None)
+            addend = skip if li % 2 == 1 else None
+            dx, dz, dw, dgn = conv_gn_bwd(d, None, ys[li], sts[li], norm.weight, x, H, W,
+                                          wT=_packed(conv.weight, "t", x.dtype) if want_dx else None, dmask=dm,
+                                          addend=addend, want_dz=(li % 2 == 0 and li > 0), rmask=rms[li])
+            skip = dz
             grads[id(conv.weight)] = dw_to_conv(dw, cin_real)
             grads[id(conv.bias)] = dgn[2]
             grads[id(norm.weight)] = dgn[0]

@@ -50,6 +50,8 @@ class RolloutBuffer:
         if obs_codes:
             if C != 10:
                 raise ValueError("obs_codes needs the env's 10-plane observation")
+            if self.device.type != "cuda":
+                raise L.MsEnvError("obs_codes buffers are encoded on the HIP device (mc_obs_encode)")
             self.obs = torch.zeros((B, H, W), dtype=torch.uint8, device=device)
         else:
             self.obs = torch.zeros((B, C, H, W), dtype=torch.float32, device=device)

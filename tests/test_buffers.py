@@ -119,3 +119,16 @@ def test_stratified_minibatches_are_world_invariant(world):
     # a different epoch seed permutes differently
     other = [set(b.actions.tolist()) for b in _tagged(N, T, 0).get_stratified_minibatches(mbs, S, 0, seed=78)]
     assert other != full
+
+
+def test_obs_codes_buffer_layout_and_cpu_guard():
+    """The u8-code buffer (the Trainer's layout) stores [B, H, W] bytes and is HIP-only: the
+    encode is a device kernel, so a CPU buffer in that mode is refused up front."""
+    from ms_amd import _lib as L
+    from ms_amd.buffers import RolloutBuffer
+    with pytest.raises(L.MsEnvError):
+        RolloutBuffer(4, 2, (10, 3, 3), 9, torch.device("cpu"), obs_codes=True)
+    with pytest.raises(ValueError):
+        RolloutBuffer(4, 2, (11, 3, 3), 9, torch.device("cpu"), obs_codes=True)
+    b = RolloutBuffer(4, 2, (10, 3, 3), 9, torch.device("cpu"))
+    assert b.obs.shape == (8, 10, 3, 3) and b.obs.dtype == torch.float32 and not b.obs_codes

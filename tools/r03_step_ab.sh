@@ -1,6 +1,8 @@
 #!/bin/bash
 # k_step A/B: the product library vs tools/bin/noplace (a fixed mine pattern instead of the
-# placement; timing only) at the headline and the 9x9 point, alternated twice.
+# placement; timing only) at the headline and the 9x9 point, alternated twice. The noplace build
+# hook was removed after the measurement; this script stays as the record of how
+# profiles/r03/k_step_noplacement_ab.txt was made.
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp

@@ -17,6 +17,7 @@ ap.add_argument("--hw", default="16x16")
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--no-torch", action="store_true")
 ap.add_argument("--bwd", action="store_true", help="also time the fused backward of the layer")
+ap.add_argument("--mask", action="store_true", help="the forward also writes the ReLU bitmask (as training does)")
 args = ap.parse_args()
 H, W = (int(v) for v in args.hw.split("x"))
 dev = torch.device("cuda")
@@ -39,7 +40,7 @@ def t(fn, iters):
 
 
 flop = 2 * n * P * 96 * 864
-f1 = t(lambda: conv_gn_fwd(x, wt, b, g, be, H, W, res=res), args.iters)
+f1 = t(lambda: conv_gn_fwd(x, wt, b, g, be, H, W, res=res, want_mask=args.mask), args.iters)
 print(f"fused conv+GN+res+ReLU  n={n} {H}x{W}: {f1 * 1e3:.2f} ms  {flop / f1 / 1e12:.0f} TFLOP/s(conv)", flush=True)
 if args.bwd:
     out, y, st = conv_gn_fwd(x, wt, b, g, be, H, W, res=res)

@@ -81,3 +81,32 @@ def test_build_model_names_and_errors():
         CNNResidualPolicy(10, stem_channels=0)
     sd = {"_orig_mod.stem.0.weight": 1, "_orig_mod.stem.0.bias": 2}
     assert set(strip_compile_prefix(sd)) == {"stem.0.weight", "stem.0.bias"}
+
+
+def test_models_take_cell_codes_on_cpu():
+    """The Trainer's rollout buffer holds u8 cell codes [N, H, W] (ms_amd.fused.obs_encode):
+    codes_to_obs decodes them to the env's one-hot planes (0 = hidden -> all zero, 1 + k = revealed
+    with k adjacent mines -> planes 0 and 1 + k), and both models give the same outputs on codes as
+    on the decoded obs (the PyTorch path; the fused path is tested on the GPU)."""
+    from ms_amd.fused import codes_to_obs
+    from ms_amd.models import build_model
+    codes = torch.arange(10, dtype=torch.uint8).view(1, 2, 5)
+    obs = codes_to_obs(codes)
+    assert obs.shape == (1, 10, 2, 5) and obs.dtype == torch.float32
+    for i in range(10):
+        r, c = divmod(i, 5)
+        want = torch.zeros(10)
+        if i > 0:
+            want[0] = 1.0
+            want[i] = 1.0
+        assert torch.equal(obs[0, :, r, c], want), i
+    g = torch.Generator().manual_seed(2)
+    codes = torch.randint(0, 10, (6, 9, 9), dtype=torch.uint8, generator=g)
+    for name, cfg in (("cnn", {}), ("cnn_residual", dict(stem_channels=16, blocks=1, dropout=0.0, value_hidden=16))):
+        torch.manual_seed(0)
+        m = build_model(name, obs_shape=(10, 9, 9), model_cfg=cfg).eval()
+        with torch.no_grad():
+            a = m(codes, return_mine=True)
+            b = m(codes_to_obs(codes), return_mine=True)
+        for x, y in zip(a, b):
+            assert torch.equal(x, y), name

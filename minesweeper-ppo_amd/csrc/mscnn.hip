@@ -30,6 +30,7 @@
 namespace mc {
 
 thread_local char g_err[256] = "";
+int g_variant[MCV_COUNT] = {0, 0};
 
 int num_cus() {
   static int ncu = 0;
@@ -406,11 +407,402 @@ int launch_fwd(const FwdParams<E>& p, hipStream_t s) {
   return MS_OK;
 }
 
+// ---------------------------------------------------------------------------------------
+// Wave-specialised forward, boards of P <= 256 pixels: ONE 512-thread workgroup per CU.
+//   waves 0-3, the conv waves: the implicit GEMM of sample it, transposed (D[co][px] =
+//     W[co][k] . X^T[k][px], so a lane holds one pixel and four consecutive channels per
+//     register quad, and the accumulators start at the bias), its GroupNorm statistics and
+//     y -> LDS; they also stream the conv weights tap by tap through a two-slot LDS ring
+//     (tap g+1 written while tap g is read; loads issued one tap ahead);
+//   waves 4-7, the memory waves: the epilogue of sample it-1 (affine, residual, ReLU, dropout;
+//     y, out and ReLU-bit stores) and the staging of sample it+1's input.
+// Two sample regions alternate: the conv waves read x(it) from region it&1 and leave y(it)
+// there; the memory waves read y(it-1) from the other region, then stage x(it+1) over it.
+// Each SIMD holds one conv and one memory wave, so the MFMA phase of one sample runs beside the
+// HBM phase of its neighbours (round 3's SQ counters showed the two independent 256-thread
+// workgroups per CU lining their phases up instead). Every wave passes the same 11 barriers per
+// iteration (loop top, 8 between taps, 2 for the statistics): the memory waves' work is laid
+// over the first taps' segments, their loads issued six segments before use.
+constexpr int YS = COUT + 8;  // y staging row stride (elements): 2-way ds_write_b64, conflict-free b128 reads
+constexpr int WS_FLOATS = COUT + 2 * COUT + 2 * 3 * COUT + 2 * WAVES * NGRP;
+
+template <int CIN>
+__host__ __device__ inline int ws_region_elems(int P) {
+  const int a = (P + 1) * cinp<CIN>(), b = P * YS;
+  return ((a > b ? a : b) + 7) & ~7;
+}
+template <int CIN>
+__host__ __device__ inline size_t ws_lds_bytes(int P) {
+  return (size_t)2 * ws_region_elems<CIN>(P) * 2 + (size_t)2 * COUT * cinp<CIN>() * 2 + (size_t)WS_FLOATS * 4;
+}
+
+template <typename E, int CIN, int NPT, bool FULL>
+__global__ __launch_bounds__(512, 1) void k_conv_gn_fwd_ws(FwdParams<E> p) {
+  typedef typename EV<E>::v8 E8;
+  typedef typename EV<E>::v4 E4;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int CINP = cinp<CIN>(), C8 = CIN / 8, KS = CIN / 16;
+  constexpr int NWC = (COUT * C8 + 255) / 256;        // 16-B weight chunks per conv thread and tap
+  constexpr int NXC = (NPT * 128 * C8 + 255) / 256;   // 16-B input chunks per memory thread
+  constexpr int NEC = NPT * 128 * (COUT / 8) / 256;   // 16-B output chunks per memory thread (6 NPT)
+  constexpr int EPS = NEC / 3;                        // of them per epilogue segment (one c8 each)
+  const int H = p.H, W = p.W, P = H * W;
+  const int REG = ws_region_elems<CIN>(P);
+  E* sReg = reinterpret_cast<E*>(smem);  // [2][REG]
+  E* sRing = sReg + 2 * REG;             // [2][COUT][CINP]
+  float* sBias = reinterpret_cast<float*>(sRing + 2 * COUT * CINP);
+  float* sGB = sBias + COUT;           // gamma | beta
+  float* sCoef = sGB + 2 * COUT;       // [2][scale | shift | dropout scale][COUT]
+  float* sRed = sCoef + 6 * COUT;      // [2 passes][WAVES][NGRP]
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
+  const int G = gridDim.x;
+  const int cnt = p.N > (int)blockIdx.x ? (p.N - 1 - (int)blockIdx.x) / G + 1 : 0;
+
+  if (wave < WAVES) {
+    // =============================== conv waves ===============================
+    const int ctid = threadIdx.x;
+    const int l32 = lane & 31, hh = lane >> 5;
+    for (int i = ctid; i < COUT; i += 256) {
+      sBias[i] = p.bias[i];
+      sGB[i] = p.gamma[i];
+      sGB[COUT + i] = p.beta[i];
+    }
+    u32x4 wr[NWC];
+    auto wload = [&](int tap) {
+      const u32x4* ws = reinterpret_cast<const u32x4*>(p.wt + (size_t)tap * COUT * CIN);
+#pragma unroll
+      for (int k = 0; k < NWC; ++k) {
+        const int i = ctid + 256 * k;
+        if (k < COUT * C8 / 256 || i < COUT * C8) wr[k] = ws[i];
+      }
+    };
+    auto wstore = [&](int slot) {
+      E* sw = sRing + slot * COUT * CINP;
+#pragma unroll
+      for (int k = 0; k < NWC; ++k) {
+        const int i = ctid + 256 * k;
+        if (k < COUT * C8 / 256 || i < COUT * C8) {
+          const int co = i / C8, c8 = i - co * C8;
+          *reinterpret_cast<u32x4*>(&sw[co * CINP + c8 * 8]) = wr[k];
+        }
+      }
+    };
+    wload(0);
+    wstore(0);
+    wload(1);
+    int qr[NPT], qc[NPT];
+    bool qv[NPT];
+#pragma unroll
+    for (int t = 0; t < NPT; ++t) {
+      const int q = (wave * NPT + t) * 32 + l32;
+      qv[t] = FULL || q < P;
+      qr[t] = qv[t] ? q / W : -1000;  // a pixel past P reads the zero row at every tap
+      qc[t] = qv[t] ? q - qr[t] * W : -1000;
+    }
+    const float inv_cnt = 1.0f / (16.0f * (float)P);
+    const int total = 9 * cnt;  // weight taps streamed by this workgroup
+    for (int it = 0; it <= cnt; ++it) {
+      const bool conv = it < cnt;
+      const int n = (int)blockIdx.x + it * G;
+      const E* sX = sReg + (it & 1) * REG;
+      float dmv = 1.f;
+      lds_barrier();  // A: x(it) staged, tap 0 in its slot
+      f32x16 acc[NPT][3];
+      if (conv) {
+        if (p.dmask && ctid < COUT) dmv = p.dmask[(size_t)n * COUT + ctid];  // used after the taps
+#pragma unroll
+        for (int ct = 0; ct < 3; ++ct)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const f32x4 b4 = *reinterpret_cast<const f32x4*>(&sBias[ct * 32 + 8 * j + 4 * hh]);
+#pragma unroll
+            for (int t = 0; t < NPT; ++t)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) acc[t][ct][4 * j + e] = b4[e];
+          }
+      }
+      for (int tap = 0; tap < 9; ++tap) {
+        if (tap) lds_barrier();  // T_tap: the ring slot of this tap is written, the other one free
+        if (!conv) continue;
+        const int g = it * 9 + tap;
+        if (g + 1 < total) wstore((g + 1) & 1);  // registers hold tap (g+1) mod 9
+        if (g + 2 < total) wload((tap + 2) % 9);
+        const E* sW = sRing + (g & 1) * COUT * CINP;
+        const int dr = tap / 3 - 1, dc = tap % 3 - 1;
+        int aoff[NPT];
+#pragma unroll
+        for (int t = 0; t < NPT; ++t) {
+          const int sr = qr[t] + dr, sc = qc[t] + dc;
+          const bool v = (unsigned)sr < (unsigned)H && (unsigned)sc < (unsigned)W;
+          aoff[t] = (v ? sr * W + sc : P) * CINP + 8 * hh;
+        }
+        E8 A[2][3], B[2][NPT];  // A: weights (32 co x 16 k), B: input (16 k x 32 px)
+        auto ld = [&](int ks, E8 (&a)[3], E8 (&b)[NPT]) {
+#pragma unroll
+          for (int ct = 0; ct < 3; ++ct)
+            a[ct] = *reinterpret_cast<const E8*>(&sW[(ct * 32 + l32) * CINP + ks * 16 + 8 * hh]);
+#pragma unroll
+          for (int t = 0; t < NPT; ++t) b[t] = *reinterpret_cast<const E8*>(&sX[aoff[t] + ks * 16]);
+        };
+        ld(0, A[0], B[0]);
+        __builtin_amdgcn_sched_group_barrier(0x100, NPT + 3, 0);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          if (ks + 1 < KS) {
+            ld(ks + 1, A[(ks + 1) & 1], B[(ks + 1) & 1]);
+            __builtin_amdgcn_sched_group_barrier(0x100, NPT + 3, 0);
+          }
+#pragma unroll
+          for (int t = 0; t < NPT; ++t)
+#pragma unroll
+            for (int ct = 0; ct < 3; ++ct) acc[t][ct] = mfma32(A[ks & 1][ct], B[ks & 1][t], acc[t][ct]);
+          __builtin_amdgcn_sched_group_barrier(0x008, 3 * NPT, 0);
+        }
+      }
+      // ---- GroupNorm statistics: group 2 ct + half = registers 8 half .. 8 half + 7 of tile ct ----
+      float gmean[NGRP], grstd[NGRP];
+      if (conv) {
+#pragma unroll
+        for (int ct = 0; ct < 3; ++ct)
+#pragma unroll
+          for (int hf = 0; hf < 2; ++hf) {
+            float v[NPT * 8];
+#pragma unroll
+            for (int t = 0; t < NPT; ++t)
+#pragma unroll
+              for (int i = 0; i < 8; ++i) v[t * 8 + i] = qv[t] ? acc[t][ct][8 * hf + i] : 0.f;
+#pragma unroll
+            for (int w2 = NPT * 4; w2 >= 1; w2 >>= 1)
+#pragma unroll
+              for (int i = 0; i < w2; ++i) v[i] += v[i + w2];
+            const float s = wave_sum(v[0]);
+            if (lane == 0) sRed[wave * NGRP + 2 * ct + hf] = s;
+          }
+      }
+      lds_barrier();  // S1: every conv wave's reads of x(it) done; pass-1 sums posted
+      if (conv) {
+#pragma unroll
+        for (int g = 0; g < NGRP; ++g) {
+          float tot = 0.f;
+#pragma unroll
+          for (int w = 0; w < WAVES; ++w) tot += sRed[w * NGRP + g];
+          gmean[g] = tot * inv_cnt;
+        }
+        // y -> LDS over x(it): four consecutive channels per register quad, one 8-B write each
+        E* sY = sReg + (it & 1) * REG;
+#pragma unroll
+        for (int t = 0; t < NPT; ++t) {
+          const int px = (wave * NPT + t) * 32 + l32;
+          if (qv[t]) {
+#pragma unroll
+            for (int ct = 0; ct < 3; ++ct)
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                E4 q4;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) q4[e] = (E)acc[t][ct][4 * j + e];
+                *reinterpret_cast<E4*>(&sY[px * YS + ct * 32 + 8 * j + 4 * hh]) = q4;
+              }
+          }
+        }
+#pragma unroll
+        for (int ct = 0; ct < 3; ++ct)
+#pragma unroll
+          for (int hf = 0; hf < 2; ++hf) {
+            const float mu = gmean[2 * ct + hf];
+            float v[NPT * 8];
+#pragma unroll
+            for (int t = 0; t < NPT; ++t)
+#pragma unroll
+              for (int i = 0; i < 8; ++i) {
+                const float d = acc[t][ct][8 * hf + i] - mu;
+                v[t * 8 + i] = qv[t] ? d * d : 0.f;
+              }
+#pragma unroll
+            for (int w2 = NPT * 4; w2 >= 1; w2 >>= 1)
+#pragma unroll
+              for (int i = 0; i < w2; ++i) v[i] += v[i + w2];
+            const float s = wave_sum(v[0]);
+            if (lane == 0) sRed[WAVES * NGRP + wave * NGRP + 2 * ct + hf] = s;
+          }
+      }
+      lds_barrier();  // S2: pass-2 sums posted
+      if (conv) {
+#pragma unroll
+        for (int g = 0; g < NGRP; ++g) {
+          float tot = 0.f;
+#pragma unroll
+          for (int w = 0; w < WAVES; ++w) tot += sRed[WAVES * NGRP + w * NGRP + g];
+          grstd[g] = rsqrtf(tot * inv_cnt + p.eps);
+        }
+        if (ctid < COUT) {  // per-channel coefficients of the memory waves' epilogue
+          const int g = ctid >> 4;
+          float mu = 0.f, rs = 0.f;
+#pragma unroll
+          for (int gg = 0; gg < NGRP; ++gg)
+            if (gg == g) {
+              mu = gmean[gg];
+              rs = grstd[gg];
+            }
+          float* co = sCoef + (it & 1) * 3 * COUT;
+          const float a = sGB[ctid] * rs;
+          co[ctid] = a;
+          co[COUT + ctid] = sGB[COUT + ctid] - mu * a;
+          co[2 * COUT + ctid] = dmv;
+          if (p.stats && ctid < NGRP) {
+            float m = 0.f, r = 0.f;
+#pragma unroll
+            for (int gg = 0; gg < NGRP; ++gg)
+              if (gg == ctid) {
+                m = gmean[gg];
+                r = grstd[gg];
+              }
+            p.stats[((size_t)n * NGRP + ctid) * 2 + 0] = m;
+            p.stats[((size_t)n * NGRP + ctid) * 2 + 1] = r;
+          }
+        }
+      }
+    }
+  } else {
+    // =============================== memory waves ===============================
+    const int mtid = threadIdx.x - 256;
+    u32x4 xr[NXC];   // the next input tile but one, in flight
+    u32x4 rq[NEC];   // the residual of the sample whose epilogue runs next
+    auto xload = [&](int n) {
+      const u32x4* xs = reinterpret_cast<const u32x4*>(p.x + (size_t)n * P * CIN);
+#pragma unroll
+      for (int k = 0; k < NXC; ++k) {
+        const int i = mtid + 256 * k;
+        if ((FULL && (k + 1) * 256 <= NPT * 128 * C8) || i < P * C8) xr[k] = xs[i];
+      }
+    };
+    auto xstore = [&](int region) {
+      E* sx = sReg + region * REG;
+#pragma unroll
+      for (int k = 0; k < NXC; ++k) {
+        const int i = mtid + 256 * k;
+        if ((FULL && (k + 1) * 256 <= NPT * 128 * C8) || i < P * C8) {
+          const int px = i / C8, c8 = i - px * C8;
+          *reinterpret_cast<u32x4*>(&sx[px * CINP + c8 * 8]) = xr[k];
+        }
+      }
+      if (mtid <= C8) *reinterpret_cast<u32x4*>(&sx[P * CINP + mtid * 8]) = u32x4{0u, 0u, 0u, 0u};  // zero row
+    };
+    auto rload = [&](int n) {
+      const u32x4* rs = reinterpret_cast<const u32x4*>(p.res + (size_t)n * P * COUT);
+#pragma unroll
+      for (int k = 0; k < NEC; ++k) {
+        const int c = mtid + 256 * k;
+        rq[k] = u32x4{0u, 0u, 0u, 0u};
+        if (FULL || c < P * (COUT / 8)) rq[k] = rs[c];
+      }
+    };
+    // epilogue segment j of sample n (its y in region rg): the chunks k = j + 3u share one
+    // channel octet cg, whose scale / shift / dropout scale are read once
+    auto epi = [&](int n, int rg, int j) {
+      const E* sY = sReg + rg * REG;
+      const float* co = sCoef + rg * 3 * COUT;
+      const int cg = (mtid % (COUT / 8) + 4 * j) % (COUT / 8);
+      float ca[8], cb[8], cd[8];
+#pragma unroll
+      for (int h4 = 0; h4 < 2; ++h4) {
+        const f32x4 a4 = *reinterpret_cast<const f32x4*>(&co[cg * 8 + 4 * h4]);
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(&co[COUT + cg * 8 + 4 * h4]);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(&co[2 * COUT + cg * 8 + 4 * h4]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          ca[4 * h4 + e] = a4[e];
+          cb[4 * h4 + e] = b4[e];
+          cd[4 * h4 + e] = d4[e];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < EPS; ++u) {
+        const int k = j + 3 * u, c = mtid + 256 * k;
+        if (FULL || c < P * (COUT / 8)) {
+          const int px = c / (COUT / 8);
+          const size_t o = (size_t)n * P * COUT + (size_t)c * 8;
+          const u32x4 yv = *reinterpret_cast<const u32x4*>(&sY[px * YS + cg * 8]);
+          if (p.ysave) *reinterpret_cast<u32x4*>(&p.ysave[o]) = yv;
+          const E8 y8 = __builtin_bit_cast(E8, yv);
+          const E8 r8 = __builtin_bit_cast(E8, rq[k]);
+          E8 o8;
+          uint32_t mb = 0u;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float z = fmaxf((float)y8[e] * ca[e] + cb[e] + (float)r8[e], 0.f);
+            o8[e] = (E)(z * cd[e]);
+            mb |= ((float)o8[e] > 0.f ? 1u : 0u) << e;
+          }
+          *reinterpret_cast<u32x4*>(&p.out[o]) = __builtin_bit_cast(u32x4, o8);
+          if (p.rmask) p.rmask[(size_t)n * P * (COUT / 8) + c] = (uint8_t)mb;
+        }
+      }
+    };
+#pragma unroll
+    for (int k = 0; k < NEC; ++k) rq[k] = u32x4{0u, 0u, 0u, 0u};
+    if (cnt > 0) {
+      xload((int)blockIdx.x);
+      xstore(0);
+      if (mtid <= C8) *reinterpret_cast<u32x4*>(&sReg[REG + P * CINP + mtid * 8]) = u32x4{0u, 0u, 0u, 0u};
+    }
+    if (cnt > 1) xload((int)blockIdx.x + G);
+    for (int it = 0; it <= cnt; ++it) {
+      const int np = (int)blockIdx.x + (it - 1) * G;  // the sample whose epilogue runs now
+      const bool ep = it >= 1;
+      const int rg = (it + 1) & 1;                    // its y; then x(it+1) is staged there
+      lds_barrier();  // A
+      if (ep) epi(np, rg, 0);
+      lds_barrier();  // T1
+      if (ep) epi(np, rg, 1);
+      lds_barrier();  // T2
+      if (ep) epi(np, rg, 2);
+      lds_barrier();  // T3: every memory wave's reads of y(it-1) done
+      lds_barrier();  // T4
+      if (it + 1 < cnt) xstore(rg);
+      lds_barrier();  // T5
+      if (it + 2 < cnt) xload((int)blockIdx.x + (it + 2) * G);
+      if (it < cnt && p.res) rload((int)blockIdx.x + it * G);
+      lds_barrier();  // T6
+      lds_barrier();  // T7
+      lds_barrier();  // T8
+      lds_barrier();  // S1
+      lds_barrier();  // S2
+    }
+  }
+}
+
+template <typename E, int CIN, int NPT, bool FULL>
+int launch_fwd_ws(const FwdParams<E>& p, hipStream_t s) {
+  const size_t lds = ws_lds_bytes<CIN>(p.H * p.W);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)k_conv_gn_fwd_ws<E, CIN, NPT, FULL>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  const int cap = num_cus();
+  const int grid = p.N < cap ? p.N : cap;
+  hipLaunchKernelGGL((k_conv_gn_fwd_ws<E, CIN, NPT, FULL>), dim3(grid), dim3(512), lds, s, p);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd launch: %s", hipGetErrorString(e));
+    return MS_EHIP;
+  }
+  return MS_OK;
+}
+
 template <typename E, int CIN>
 int dispatch_fwd(const FwdParams<E>& p, hipStream_t s) {
   const int P = p.H * p.W;
   const int tiles = (P + 31) / 32;
   const int npt = (tiles + WAVES - 1) / WAVES;
+  if (P <= 256 && g_variant[MCV_FWD] != 1) {
+    if (P == 256) return launch_fwd_ws<E, CIN, 2, true>(p, s);
+    if (P > 128) return launch_fwd_ws<E, CIN, 2, false>(p, s);
+    return launch_fwd_ws<E, CIN, 1, false>(p, s);
+  }
   if (P == 256) return launch_fwd<E, CIN, 2, true>(p, s);
   switch (npt) {
     case 1: return launch_fwd<E, CIN, 1, false>(p, s);
@@ -524,6 +916,15 @@ int run_fwd(const uint16_t* x, const uint16_t* w, const float* bias, const float
 extern "C" {
 
 const char* mc_last_error(void) { return g_err; }
+
+int mc_set_variant(int32_t kernel, int32_t variant) {
+  if (kernel < 0 || kernel >= MCV_COUNT || variant < 0 || variant > 2) {
+    snprintf(g_err, sizeof g_err, "mc_set_variant: bad kernel %d / variant %d", kernel, variant);
+    return MS_EINVAL;
+  }
+  g_variant[kernel] = variant;
+  return MS_OK;
+}
 
 int mc_obs_encode(const float* obs, uint8_t* codes, uint16_t* nhwc, int64_t n, int32_t a, int32_t cin_pad,
                   int32_t dtype, void* stream) {

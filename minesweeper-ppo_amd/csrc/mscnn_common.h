@@ -16,6 +16,8 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 // native vector: HIP's uint4 struct copies through memcpy and is left in scratch
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 // 16-bit activation / weight element: __bf16 (bf16 autocast) or _Float16 (fp16 autocast,
@@ -90,6 +92,16 @@ __device__ __forceinline__ int opaque0() {
 // prefetched loads at every barrier. The memory clobber keeps the compiler from moving
 // memory operations across it.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// sum over the whole wave, returned in every lane (row sums, then the four rows' last lanes)
+__device__ __forceinline__ float wave_sum(float v) {
+  v = row_sum16(v);
+  return (readlane_f(v, 15) + readlane_f(v, 31)) + (readlane_f(v, 47) + readlane_f(v, 63));
+}
+
+// Kernel variants (msenv_debug.h mc_set_variant): 0 = the dispatcher's choice.
+enum { MCV_FWD = 0, MCV_BWD = 1, MCV_COUNT = 2 };
+extern int g_variant[MCV_COUNT];
 
 __device__ __forceinline__ bf16x8 cat8(bf16x4 lo, bf16x4 hi) {
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};

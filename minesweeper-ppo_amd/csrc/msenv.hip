@@ -1151,7 +1151,8 @@ __device__ void place_serial_packed(Pcg& rng, uint32_t& mine_out, const Block& B
 
 template <int H_, int W_>
 constexpr bool packable() {
-  return H_ >= 1 && H_ <= 16 && W_ >= 1 && W_ <= 31 && H_ * W_ <= 128;
+  // W_ <= 30: pk_emit's neighbour count shifts a u32 row by up to W_ + 1 bits
+  return H_ >= 1 && H_ <= 16 && W_ >= 1 && W_ <= 30 && H_ * W_ <= 128;
 }
 
 // MS_DIAG builds: per-board phase stamps into this env's diag row (lane r == 0 of the board)

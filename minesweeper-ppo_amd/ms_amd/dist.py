@@ -50,15 +50,3 @@ def broadcast_module(module: torch.nn.Module, info: DistInfo) -> None:
     if info.world > 1:
         for t in list(module.parameters()) + list(module.buffers()):
             dist.broadcast(t.data, src=0, group=info.group)
-
-
-def all_reduce_mean_(t: torch.Tensor, info: DistInfo) -> torch.Tensor:
-    if info.world > 1:
-        dist.all_reduce(t, group=info.group)
-        t.div_(info.world)
-    return t
-
-
-def env_shard(num_envs_total: int, info: DistInfo) -> tuple[int, int]:
-    assert num_envs_total % info.world == 0, "num_envs must divide evenly across ranks"
-    return info.rank, info.world

@@ -46,6 +46,26 @@ def _check(rc):
         raise L.MsEnvError(lib.mc_last_error().decode(errors="replace"))
 
 
+VARIANT_FWD, VARIANT_BWD = 0, 1  # mc_set_variant kernels (include/msenv_debug.h)
+
+
+class kernel_variant:
+    """Context manager: run mc_conv_gn_fwd (kernel 0) or mc_conv_gn_bwd (kernel 1) on one
+    variant -- 0 the dispatcher's choice, 1 the per-sample kernel, 2 the wave-specialised
+    kernel -- for parity tests of every path and same-process A/B timing."""
+
+    def __init__(self, kernel: int, variant: int):
+        self.kernel, self.variant = kernel, variant
+
+    def __enter__(self):
+        _check(_fn("mc_set_variant", [_i32, _i32])(self.kernel, self.variant))
+        return self
+
+    def __exit__(self, *exc):
+        _check(_fn("mc_set_variant", [_i32, _i32])(self.kernel, 0))
+        return False
+
+
 def prep_weight(w: torch.Tensor, cin_pad: int, dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
     """[96, cin, 3, 3] (f32 nn.Conv2d weight) -> ``dtype`` [9, 96, cin_pad], tap = 3*ky + kx."""
     co, ci = w.shape[0], w.shape[1]

@@ -71,7 +71,8 @@ class _ResidualBlock(nn.Module):
     def forward(self, x: torch.Tensor, dmask: Optional[torch.Tensor] = None) -> torch.Tensor:
         y = self.act(self.norm1(self.conv1(x)))
         # dmask: keyed Dropout2d mask [N, C] (keep / (1 - p)), in place of the torch-RNG draw
-        y = y * dmask.to(y.dtype)[:, :, None, None] if dmask is not None else self.dropout(y)
+        # (the scale multiplies in f32 and only the product is rounded, as nn.Dropout2d does)
+        y = (y.float() * dmask.float()[:, :, None, None]).to(y.dtype) if dmask is not None else self.dropout(y)
         y = self.norm2(self.conv2(y))
         return self.act(y + x)
 

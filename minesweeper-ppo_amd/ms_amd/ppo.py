@@ -25,6 +25,8 @@ import torch
 import torch.distributed as dist
 import torch.nn.functional as F
 
+from .profiling import prange
+
 
 @dataclass
 class PPOConfig:
@@ -141,7 +143,11 @@ def ppo_losses(model, batch, cfg: PPOConfig, amp_dtype: Optional[torch.dtype] = 
         if need_mine and getattr(batch, "mine_labels", None) is not None and mine_logits is not None:
             # masked sums instead of boolean gathers: no host sync (the reference's
             # lf[mask] + float(pos_weight) sync twice per minibatch, ppo.py:64-71)
-            lf = mine_logits.squeeze(1).float()
+            # under 16-bit autocast the reference's mine logits are 16-bit tensors: its pos_weight is
+            # rounded to their dtype (ppo.py:70) and its calibration sigmoid runs in it (ppo.py:78-79)
+            amp16 = batch.obs.is_cuda and amp_dtype in (torch.float16, torch.bfloat16)
+            lf16 = mine_logits.squeeze(1).to(amp_dtype) if amp16 else mine_logits.squeeze(1)
+            lf = lf16.float()
             y = batch.mine_labels
             vmask = getattr(batch, "mine_valid", None)
             vm = torch.ones_like(y) if vmask is None else vmask.to(y.dtype)
@@ -152,12 +158,14 @@ def ppo_losses(model, batch, cfg: PPOConfig, amp_dtype: Optional[torch.dtype] = 
             scale = world / cnt.clamp_min(1.0)  # empty valid set -> 0 loss (ppo.py:82-87)
             if cfg.aux_mine_weight > 0:
                 pw = (cnt - pos + 1e-6) / (pos + 1e-6)
+                if amp16:
+                    pw = pw.to(amp_dtype).float()
                 bce = F.binary_cross_entropy_with_logits(lf, y, pos_weight=pw, reduction="none")
                 aux_bce = (bce * vm).sum() * scale
                 loss = loss + cfg.aux_mine_weight * aux_bce
                 out["aux_bce"] = aux_bce
             if cfg.aux_mine_calib_weight > 0:
-                calib = ((torch.sigmoid(lf) - y).pow(2) * vm).sum() * scale
+                calib = ((torch.sigmoid(lf16).float() - y).pow(2) * vm).sum() * scale
                 loss = loss + cfg.aux_mine_calib_weight * calib
                 out["aux_calib"] = calib
         if cfg.beta_l2 > 0 and hasattr(model, "beta_regularizer"):
@@ -175,30 +183,37 @@ def ppo_update(model, optimizer, batch, cfg: PPOConfig, scaler=None, *,
     ``flat_grads``: the gradient all-reduce runs over its flat bucket."""
     if group is not None and flat_grads is None:
         raise ValueError("ppo_update(group=...) needs flat_grads=FlatGrads(model.parameters())")
-    out = ppo_losses(model, batch, cfg, amp_dtype=amp_dtype, group=group)
+    with prange("ppo/forward"):
+        out = ppo_losses(model, batch, cfg, amp_dtype=amp_dtype, group=group)
     loss = out["loss"]
     if flat_grads is not None:
         flat_grads.zero()
     else:
         optimizer.zero_grad(set_to_none=True)
     if scaler is not None and batch.obs.is_cuda:
-        scaler.scale(loss).backward()
+        with prange("ppo/backward"):
+            scaler.scale(loss).backward()
         if flat_grads is not None:
             flat_grads.release_unused()
         if group is not None:
-            flat_grads.all_reduce_mean(group)
-        scaler.unscale_(optimizer)
-        torch.nn.utils.clip_grad_norm_(model.parameters(), cfg.max_grad_norm)
-        scaler.step(optimizer)
-        scaler.update()
+            with prange("ppo/all_reduce"):
+                flat_grads.all_reduce_mean(group)
+        with prange("ppo/optimizer"):
+            scaler.unscale_(optimizer)
+            torch.nn.utils.clip_grad_norm_(model.parameters(), cfg.max_grad_norm)
+            scaler.step(optimizer)
+            scaler.update()
     else:
-        loss.backward()
+        with prange("ppo/backward"):
+            loss.backward()
         if flat_grads is not None:
             flat_grads.release_unused()
         if group is not None:
-            flat_grads.all_reduce_mean(group)
-        torch.nn.utils.clip_grad_norm_(model.parameters(), cfg.max_grad_norm)
-        optimizer.step()
+            with prange("ppo/all_reduce"):
+                flat_grads.all_reduce_mean(group)
+        with prange("ppo/optimizer"):
+            torch.nn.utils.clip_grad_norm_(model.parameters(), cfg.max_grad_norm)
+            optimizer.step()
     stats = {k: v.detach().float() for k, v in out.items()}
     if sync_stats:
         keys = sorted(stats)

@@ -28,6 +28,7 @@ from . import _lib as L
 from .buffers import RolloutBuffer
 from .dropout import ROLLOUT, keyed_dropout, mix_seed
 from .env import OBS_CHANNELS, VecMinesweeper
+from .profiling import PhaseTimer, RolloutTimings, prange
 
 
 def sample_masked(logits: torch.Tensor, mask: torch.Tensor, seed: int, counter: int,
@@ -59,9 +60,11 @@ def _autocast(device: torch.device, amp_dtype):
 def collect_rollout(vec: VecMinesweeper, model: torch.nn.Module, steps: int, device: torch.device,
                     aux_mine_weight: float = 0.0, aux_mine_calib_weight: float = 0.0, *,
                     amp_dtype: Optional[torch.dtype] = torch.bfloat16, buffer: Optional[RolloutBuffer] = None,
-                    sample_seed: int = 0, sample_counter: int = 0, obs_codes: bool = False
+                    sample_seed: int = 0, sample_counter: int = 0, obs_codes: bool = False, timing: bool = True
                     ) -> Tuple[RolloutBuffer, Dict]:
-    """Same contract as the reference: returns (buffer, {"last_values", "timings"}).
+    """Same contract as the reference: returns (buffer, {"last_values", "timings"}); ``timings`` has
+    the reference's keys (train_rl.py:278-288), timed on the GPU with HIP events and resolved (one
+    host sync) on first read (ms_amd.profiling.RolloutTimings); ``timing=False`` records no events.
     ``buffer`` may be passed back in to reuse its HBM (2.7 GB at N=4096, T=64; 67 MB with
     ``obs_codes``: the buffer then holds u8 cell codes, the env's obs going through a
     one-step scratch and ms_amd.fused.obs_encode)."""
@@ -79,6 +82,7 @@ def collect_rollout(vec: VecMinesweeper, model: torch.nn.Module, steps: int, dev
     env_ids = torch.arange(vec.env_begin, vec.env_begin + N, dtype=torch.int64, device=device)
     dseed = mix_seed(sample_seed, ROLLOUT)
     t0 = time.perf_counter()
+    tm = PhaseTimer(device, enabled=timing)
     s0 = buffer.slot(0)
     last_obs = torch.empty((N, OBS_CHANNELS, H, W), dtype=torch.float32, device=device)
     last_mask = torch.empty((N, H * W), dtype=torch.bool, device=device)
@@ -86,31 +90,40 @@ def collect_rollout(vec: VecMinesweeper, model: torch.nn.Module, steps: int, dev
     vec.reset(out={"obs": last_obs if buffer.obs_codes else s0["obs"], "action_mask": s0["action_mask"]})
     if buffer.obs_codes:
         obs_encode(last_obs, s0["obs"])
+    tm.start()
     for t in range(steps):
         s = buffer.slot(t)
         if need_aux:
-            vec.mine_labels(s["mine_labels"], s["mine_valid"])
-        with _autocast(device, amp_dtype), \
-                keyed_dropout(model, env_ids + t * vec.num_envs_total, dseed, sample_counter + t):
-            logits, values = model(s["obs"])
-        sample_masked(logits, s["action_mask"], sample_seed, sample_counter + t, s["actions"], s["logp"],
-                      row_begin=vec.env_begin)
+            with prange("rollout/labels"):
+                vec.mine_labels(s["mine_labels"], s["mine_valid"])
+            tm.split("mine_label_copy")
+        with prange("rollout/forward"):
+            with _autocast(device, amp_dtype), \
+                    keyed_dropout(model, env_ids + t * vec.num_envs_total, dseed, sample_counter + t):
+                logits, values = model(s["obs"])
+            sample_masked(logits, s["action_mask"], sample_seed, sample_counter + t, s["actions"], s["logp"],
+                          row_begin=vec.env_begin)
+        tm.split("model_forward")
         s["values"].copy_(values.float())
+        tm.split("tensor_bridge")
         if t + 1 < steps:
             nxt = buffer.slot(t + 1)
             out = {"obs": last_obs if buffer.obs_codes else nxt["obs"], "action_mask": nxt["action_mask"]}
         else:
             out = {"obs": last_obs, "action_mask": last_mask}
         out["rewards"], out["dones"] = s["rewards"], s["dones"]
-        vec.step(s["actions"], out=out)
+        with prange("rollout/env_step"):
+            vec.step(s["actions"], out=out)
+        tm.split("env_step")
         if buffer.obs_codes and t + 1 < steps:
             obs_encode(last_obs, nxt["obs"])
-    with _autocast(device, amp_dtype), \
+            tm.split("tensor_bridge")
+    with prange("rollout/bootstrap"), _autocast(device, amp_dtype), \
             keyed_dropout(model, env_ids + steps * vec.num_envs_total, dseed, sample_counter + steps):
         _, last_values = model(last_obs)
     last_values = last_values.float()
     buffer._t = steps
-    timings = {"steps": steps, "enqueue_total_s": time.perf_counter() - t0}
+    timings = RolloutTimings(steps, tm, time.perf_counter() - t0)
     return buffer, {"last_values": last_values, "timings": timings, "last_obs": last_obs,
                     "last_mask": last_mask}
 

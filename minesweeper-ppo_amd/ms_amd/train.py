@@ -36,6 +36,7 @@ from .dropout import MINIBATCH, keyed_dropout, mix_seed
 from .env import EnvConfig, VecMinesweeper
 from .models import build_model, strip_compile_prefix
 from .ppo import FlatGrads, PPOConfig, ppo_update
+from .profiling import prange
 from .rollout import collect_rollout
 
 
@@ -221,12 +222,15 @@ class Trainer:
         pc.aux_mine_weight = aux_weight_at(update, cfg.total_updates, self.aux_base, self.aux_warm_w,
                                            self.aux_final_w, self.aux_warm_u, self.aux_power)
         self.model.train()
-        self.buffer, aux = collect_rollout(
-            self.vec, self.model, cfg.steps_per_env, self.device, pc.aux_mine_weight,
-            pc.aux_mine_calib_weight, amp_dtype=self.amp_dtype, buffer=self.buffer,
-            sample_seed=self.seed * 7919 + 17, sample_counter=update << 20, obs_codes=self.obs_codes)
+        with prange("update/rollout"):
+            self.buffer, aux = collect_rollout(
+                self.vec, self.model, cfg.steps_per_env, self.device, pc.aux_mine_weight,
+                pc.aux_mine_calib_weight, amp_dtype=self.amp_dtype, buffer=self.buffer,
+                sample_seed=self.seed * 7919 + 17, sample_counter=update << 20, obs_codes=self.obs_codes,
+                timing=profile)
         mark()
-        self.buffer.compute_gae(aux["last_values"], gamma=cfg.gamma, lam=cfg.gae_lambda)
+        with prange("update/gae"):
+            self.buffer.compute_gae(aux["last_values"], gamma=cfg.gamma, lam=cfg.gae_lambda)
         mark()
         acc: Dict[str, torch.Tensor] = {}
         n = 0
@@ -237,11 +241,12 @@ class Trainer:
                                                          seed=(self.seed * 1000003 + update) * 64 + epoch)
             for k, batch in enumerate(mbs):
                 # Dropout2d masks keyed by (update, epoch, minibatch, global sample id)
-                with keyed_dropout(self.model, batch.rows, dseed, (((update << 8) + epoch) << 16) + k):
+                with prange("update/minibatch"), \
+                        keyed_dropout(self.model, batch.rows, dseed, (((update << 8) + epoch) << 16) + k):
                     st = ppo_update(self.model, self.opt, batch, pc, self.scaler, amp_dtype=self.amp_dtype,
                                     group=group, flat_grads=self.flat, sync_stats=False)
-                for k, v in st.items():
-                    acc[k] = acc[k] + v if k in acc else v
+                for name, v in st.items():
+                    acc[name] = acc[name] + v if name in acc else v
                 n += 1
         self.sched.step()
         keys = sorted(acc)
@@ -253,6 +258,9 @@ class Trainer:
             mark()
             out["rollout_s"], out["gae_s"], out["ppo_s"] = (tick[1] - tick[0], tick[2] - tick[1],
                                                            tick[3] - tick[2])
+            for key, v in aux["timings"].items():  # the reference's rollout buckets (train_rl.py:278-288)
+                if key.endswith("_total_s"):
+                    out["rollout_" + key] = v
         return out
 
     def checkpoint(self, path: str, metric=None) -> None:

@@ -45,9 +45,19 @@ PROD = [pytest.param(16, 16, 96, 32768, id="c2-16x16-32768"), pytest.param(16, 1
                                        (16, 30, 96, 9), (5, 7, 16, 3)] + PROD)
 @pytest.mark.parametrize("with_res", [False, True])
 @pytest.mark.parametrize("dt", DT)
-def test_conv_gn_fwd_matches_torch(gpu, H, W, cin, n, with_res, dt):
+@pytest.mark.parametrize("variant", [0, 1], ids=["dispatch", "per-sample"])
+def test_conv_gn_fwd_matches_torch(gpu, H, W, cin, n, with_res, dt, variant):
     """The fused forward (conv + bias + GroupNorm + affine [+ residual] + ReLU [+ dropout
-    scale]) and its ReLU bitmask vs a torch fp32 reference of the same op."""
+    scale]) and its ReLU bitmask vs a torch fp32 reference of the same op; for boards of
+    P <= 256 the dispatcher runs the wave-specialised kernel, variant 1 the per-sample one."""
+    from ms_amd.fused import VARIANT_FWD, kernel_variant
+    if variant == 1 and H * W > 256:
+        pytest.skip("P > 256 runs the per-sample kernel either way")
+    with kernel_variant(VARIANT_FWD, variant):
+        _fwd_case(gpu, H, W, cin, n, with_res, dt)
+
+
+def _fwd_case(gpu, H, W, cin, n, with_res, dt):
     from ms_amd.fused import conv_gn_fwd, prep_weight
     torch.manual_seed(0)
     P = H * W
@@ -67,6 +77,34 @@ def test_conv_gn_fwd_matches_torch(gpu, H, W, cin, n, with_res, dt):
     # the ReLU bitmask is exactly out > 0 (bit j of byte c8 = channel 8*c8 + j)
     bits = (rm.to(torch.int32)[..., None] >> torch.arange(8, device=gpu, dtype=torch.int32)) & 1
     assert torch.equal(bits.reshape(n, P, 96).bool(), out.float() > 0)
+
+
+@pytest.mark.parametrize("H,W,cin,n", [(16, 16, 96, 2000), (16, 16, 16, 700), (9, 9, 96, 900), (12, 12, 96, 300),
+                                       (5, 7, 16, 5)])
+@pytest.mark.parametrize("dt", DT)
+def test_fwd_wave_specialised_equals_per_sample(gpu, H, W, cin, n, dt):
+    """The wave-specialised forward against the per-sample kernel on the same inputs: y, the
+    statistics and out agree up to the order of the f32 sums (the bias enters the accumulators
+    first instead of last: at most one 16-bit rounding step apart), and with more samples than
+    CUs every workgroup runs several iterations of its region / weight-ring alternation."""
+    from ms_amd.fused import VARIANT_FWD, conv_gn_fwd, kernel_variant, prep_weight
+    torch.manual_seed(5)
+    P = H * W
+    x = (torch.randn(n, P, cin, device=gpu) * 0.5).to(dt)
+    w = prep_weight(torch.randn(96, cin, 3, 3, device=gpu) * (1.0 / (3 * cin ** 0.5)), cin, dt)
+    b, g, be = torch.randn(96, device=gpu) * 0.1, 1 + 0.1 * torch.randn(96, device=gpu), 0.1 * torch.randn(96, device=gpu)
+    res = torch.randn(n, P, 96, device=gpu).to(dt)
+    dmask = (torch.rand(n, 96, device=gpu) > 0.05).float() / 0.95
+    outs = []
+    for var in (1, 2):
+        with kernel_variant(VARIANT_FWD, var):
+            outs.append(conv_gn_fwd(x, w, b, g, be, H, W, res=res, dmask=dmask, want_mask=True))
+    (o1, y1, s1, m1), (o2, y2, s2, m2) = outs
+    step = 2.0 ** -7 if dt == torch.bfloat16 else 2.0 ** -10
+    assert ((y1.float() - y2.float()).abs() <= step * y1.float().abs() + 1e-6).all()
+    torch.testing.assert_close(s1, s2, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(o1.float(), o2.float(), atol=4 * step, rtol=2 * step)
+    assert (m1 != m2).float().mean().item() < 1e-3  # ReLU flips only where z ~ 0
 
 
 def _rel(a, b):

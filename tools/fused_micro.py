@@ -9,7 +9,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "minesweeper-ppo_amd"))
 import torch  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
-from ms_amd.fused import conv_gn_bwd, conv_gn_fwd, prep_weight, prep_weight_t  # noqa: E402
+from ms_amd.fused import (VARIANT_BWD, VARIANT_FWD, conv_gn_bwd, conv_gn_fwd, kernel_variant,  # noqa: E402
+                          prep_weight, prep_weight_t)
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=32768)
@@ -18,6 +19,8 @@ ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--no-torch", action="store_true")
 ap.add_argument("--bwd", action="store_true", help="also time the fused backward of the layer")
 ap.add_argument("--mask", action="store_true", help="the forward also writes the ReLU bitmask (as training does)")
+ap.add_argument("--variants", default="0", help="comma list of mc_set_variant values to time in turn "
+                "(0 dispatcher, 1 per-sample, 2 wave-specialised), e.g. 1,2,1,2")
 args = ap.parse_args()
 H, W = (int(v) for v in args.hw.split("x"))
 dev = torch.device("cuda")
@@ -40,15 +43,18 @@ def t(fn, iters):
 
 
 flop = 2 * n * P * 96 * 864
-f1 = t(lambda: conv_gn_fwd(x, wt, b, g, be, H, W, res=res, want_mask=args.mask), args.iters)
-print(f"fused conv+GN+res+ReLU  n={n} {H}x{W}: {f1 * 1e3:.2f} ms  {flop / f1 / 1e12:.0f} TFLOP/s(conv)", flush=True)
-if args.bwd:
-    out, y, st = conv_gn_fwd(x, wt, b, g, be, H, W, res=res)
-    dout = torch.randn_like(out)
-    wT = prep_weight_t(w)
-    fb = t(lambda: conv_gn_bwd(dout, out, y, st, g, x, H, W, wT=wT, addend=res, want_dz=True), args.iters)
-    print(f"fused bwd (GN-bwd + dgrad + wgrad) n={n} {H}x{W}: {fb * 1e3:.2f} ms  {2 * flop / fb / 1e12:.0f} TFLOP/s",
-          flush=True)
+for var in (int(v) for v in args.variants.split(",")):
+    with kernel_variant(VARIANT_FWD, var), kernel_variant(VARIANT_BWD, var):
+        f1 = t(lambda: conv_gn_fwd(x, wt, b, g, be, H, W, res=res, want_mask=args.mask), args.iters)
+        print(f"[variant {var}] fused conv+GN+res+ReLU  n={n} {H}x{W}: {f1 * 1e3:.3f} ms  "
+              f"{flop / f1 / 1e12:.0f} TFLOP/s(conv)", flush=True)
+        if args.bwd:
+            out, y, st = conv_gn_fwd(x, wt, b, g, be, H, W, res=res)
+            dout = torch.randn_like(out)
+            wT = prep_weight_t(w)
+            fb = t(lambda: conv_gn_bwd(dout, out, y, st, g, x, H, W, wT=wT, addend=res, want_dz=True), args.iters)
+            print(f"[variant {var}] fused bwd (GN-bwd + dgrad + wgrad) n={n} {H}x{W}: {fb * 1e3:.3f} ms  "
+                  f"{2 * flop / fb / 1e12:.0f} TFLOP/s", flush=True)
 if args.no_torch:
     sys.exit(0)
 xn = x.float().view(n, H, W, 96).permute(0, 3, 1, 2).contiguous().to(torch.bfloat16)

@@ -130,7 +130,7 @@ def test_conv_gn_bwd_matches_torch(gpu, H, W, cin, n, with_res, dt):
     storage of dy / dz / dx is 2^-9 relative; all sums are f32).
     Loose check: a full fp32 recompute from x, relative L2 <= 6e-2 (ReLU-mask flips
     where z ~ 0 between bf16 and fp32 activations dominate)."""
-    from ms_amd.fused import conv_gn_bwd, conv_gn_fwd, dw_to_conv, prep_weight, prep_weight_t
+    from ms_amd.fused import VARIANT_BWD, conv_gn_bwd, conv_gn_fwd, dw_to_conv, kernel_variant, prep_weight, prep_weight_t
     torch.manual_seed(1)
     P = H * W
     x = (torch.randn(n, P, cin, device=gpu) * (0.5 if cin == 96 else 1.0)).to(dt)
@@ -140,19 +140,23 @@ def test_conv_gn_bwd_matches_torch(gpu, H, W, cin, n, with_res, dt):
     b, g, be = torch.randn(96, device=gpu) * 0.1, 1 + 0.1 * torch.randn(96, device=gpu), 0.1 * torch.randn(96, device=gpu)
     res = torch.randn(n, P, 96, device=gpu).to(dt) if with_res else None
     dmask = ((torch.rand(n, 96, device=gpu) > 0.1).float() / 0.9) if not with_res else None
-    out, y, st = conv_gn_fwd(x, prep_weight(w, cin, dt), b, g, be, H, W, res=res, dmask=dmask)
+    out, y, st, rm = conv_gn_fwd(x, prep_weight(w, cin, dt), b, g, be, H, W, res=res, dmask=dmask, want_mask=True)
     dout = torch.randn(n, P, 96, device=gpu).to(dt)
     want_dx = cin == 96
     add = torch.randn(n, P, cin, device=gpu).to(dt) if (with_res and want_dx) else None
-    dx, dz, dw, dgn = conv_gn_bwd(dout, out, y, st, g, x, H, W, wT=prep_weight_t(w, dt) if want_dx else None,
-                                  dmask=dmask, addend=add, want_dz=with_res)
+    wT = prep_weight_t(w, dt) if want_dx else None
+    # the production path: the forward's ReLU bitmask (the wave-specialised kernel where it applies)
+    dx, dz, dw, dgn = conv_gn_bwd(dout, None, y, st, g, x, H, W, wT=wT, dmask=dmask, addend=add, want_dz=with_res,
+                                  rmask=rm)
     assert dx is None or dx.dtype == dt
-    # the bitmask path (what the trunk uses) gives bit-identical gradients
-    rm = conv_gn_fwd(x, prep_weight(w, cin, dt), b, g, be, H, W, res=res, dmask=dmask, want_mask=True)[3]
-    got = conv_gn_bwd(dout, None, y, st, g, x, H, W, wT=prep_weight_t(w, dt) if want_dx else None,
-                      dmask=dmask, addend=add, want_dz=with_res, rmask=rm)
-    for a_, b_ in zip((dx, dz, dw, dgn), got):
+    with kernel_variant(VARIANT_BWD, 1):  # the per-sample kernel: bitmask and out give bit-identical gradients
+        ref_rm = conv_gn_bwd(dout, None, y, st, g, x, H, W, wT=wT, dmask=dmask, addend=add, want_dz=with_res, rmask=rm)
+        ref_out = conv_gn_bwd(dout, out, y, st, g, x, H, W, wT=wT, dmask=dmask, addend=add, want_dz=with_res)
+    for a_, b_ in zip(ref_rm, ref_out):
         assert (a_ is None and b_ is None) or torch.equal(a_, b_)
+    # wave-specialised vs per-sample: the same sums in another order (channel sums folded 21 -> 11)
+    for a_, b_ in zip((dx, dz, dw, dgn), ref_rm):
+        assert (a_ is None and b_ is None) or _rel(a_, b_) < 2e-3
     nchw = lambda t, c: t.float().view(n, H, W, c).permute(0, 3, 1, 2).contiguous()  # noqa: E731
     nhwc = lambda t: t.permute(0, 2, 3, 1).reshape(n, P, -1)  # noqa: E731
     xr = nchw(x, cin)

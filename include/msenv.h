@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MSENV_ABI_VERSION 2
+#define MSENV_ABI_VERSION 3
 
 enum {
   MS_OK = 0,
@@ -103,6 +103,15 @@ int ms_step(ms_handle* h, const int64_t* actions, float* obs, uint8_t* mask,
 int ms_step_i32(ms_handle* h, const int32_t* actions, float* obs, uint8_t* mask,
                 float* reward, uint8_t* done, int32_t* step, int32_t* last_new,
                 double* revealed_frac, int8_t* outcome, void* stream);
+
+/* ms_step for the training rollout's buffer (no reference counterpart: the reference buffer
+ * stores the f32 one-hot obs, buffers.py:24-36): instead of obs f32[env_count,10,H,W] it writes
+ * the cell codes u8[env_count,H*W] -- 0 hidden, 1 + k revealed with k adjacent mines, the obs's
+ * one-hot planes as one byte (mscnn.h mc_obs_encode reads an obs into the same codes) -- 40x
+ * fewer bytes. codes must be 4-byte aligned when H*W % 4 == 0. Other outputs as ms_step. */
+int ms_step_codes(ms_handle* h, const int64_t* actions, uint8_t* codes, uint8_t* mask,
+                  float* reward, uint8_t* done, int32_t* step, int32_t* last_new,
+                  double* revealed_frac, int8_t* outcome, void* stream);
 
 /* Replaces the per-env label loop of collect_rollout (train_rl.py:203-219):
  * mine_labels f32[env_count,H,W] = mine_mask if first_click_done else 0;

@@ -73,6 +73,7 @@ struct KParams {
   const uint64_t* jump;  // [64][4] PCG64 jump-ahead table {A_hi, A_lo, C_hi, C_lo}, k = 1..64
   uint64_t* diag;        // MS_DIAG builds only: per-env s_memtime stamps [n][8]
   uint32_t dbg_flags;    // MS_DBG_* (msenv_debug.h)
+  uint8_t* codes;        // [n,A] cell codes (ms_step_codes: 0 hidden, 1 + k revealed with k), or NULL
 };
 
 // ---------------------------------------------------------------------------
@@ -268,10 +269,13 @@ __device__ __forceinline__ uint32_t cell_code(const uint64_t* sR, const uint64_t
 // Writes obs [10,A] f32 and mask [A] u8 of one env from the LDS rows. (sCode: A bytes of
 // this wave's LDS scratch, reserved for a code-staged emit; a flat 8-B stream of the
 // env's 10*A floats measured slower on 9x9 than the per-cell stores below.)
+// codes (may be NULL): the cell codes of the obs (1 + count where plane 1 + count is set; the
+// unreachable code 10 -- revealed before the first click, plane 0 only -- becomes 0, as
+// mc_obs_encode reads such an obs), 4-B aligned when A % 4 == 0.
 template <int H_, int W_>
 __device__ __forceinline__ void emit_obs(float* __restrict__ obs, uint8_t* __restrict__ mask,
-                                         const uint64_t* sR, const uint64_t* sM, bool fc,
-                                         const Geo<H_, W_>& g, int lane, uint8_t* sCode) {
+                                         uint8_t* __restrict__ codes, const uint64_t* sR, const uint64_t* sM,
+                                         bool fc, const Geo<H_, W_>& g, int lane, uint8_t* sCode) {
   const int A = g.A(), W = g.W;
   if ((A & 3) == 0) {
     const int nq = A >> 2;
@@ -318,6 +322,12 @@ __device__ __forceinline__ void emit_obs(float* __restrict__ obs, uint8_t* __res
                            ((code[2] ? 0u : 1u) << 16) | ((code[3] ? 0u : 1u) << 24);
         reinterpret_cast<uint32_t*>(mask)[q] = m;
       }
+      if (codes) {
+        uint32_t cw = 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cw |= (code[k] == 10u ? 0u : code[k]) << (8 * k);
+        reinterpret_cast<uint32_t*>(codes)[q] = cw;
+      }
     }
   } else {
     (void)sCode;
@@ -330,6 +340,7 @@ __device__ __forceinline__ void emit_obs(float* __restrict__ obs, uint8_t* __res
         for (uint32_t ch = 1; ch < 10; ++ch) obs[ch * A + i] = code == ch ? 1.f : 0.f;
       }
       if (mask) mask[i] = code ? 0 : 1;
+      if (codes) codes[i] = (uint8_t)(code == 10u ? 0u : code);
     }
   }
 }
@@ -951,10 +962,10 @@ __global__ __launch_bounds__(64 * EPW) void k_step(KParams p) {
 
   // ---- observation + action mask (env.py:172-196), issued before the state write-back:
   // the obs stores are ~97 % of the bytes and the launch ends when they drain ----
-  if (p.obs || p.mask) {
+  if (p.obs || p.mask || p.codes) {
     stage_rows(sR, sM, rev, mine, g, lane);
-    emit_obs(p.obs ? p.obs + env * 10 * A : nullptr, p.mask ? p.mask + env * A : nullptr, sR, sM,
-             fc, g, lane, reinterpret_cast<uint8_t*>(sTab));
+    emit_obs(p.obs ? p.obs + env * 10 * A : nullptr, p.mask ? p.mask + env * A : nullptr,
+             p.codes ? p.codes + env * A : nullptr, sR, sM, fc, g, lane, reinterpret_cast<uint8_t*>(sTab));
   }
   // ---- persist state ----
   store_meta(mp, rng, step_count, fc, lane);
@@ -1782,10 +1793,10 @@ __device__ __forceinline__ void late_env(const KParams& p, Pcg& L, const LateCfg
   store_rows(mwords, mine, sR, g, lane);
   store_rows(rwords, rev, sR, g, lane);
   __syncthreads();
-  if (p.obs || p.mask) {
+  if (p.obs || p.mask || p.codes) {
     stage_rows(sR, sM, rev, mine, g, lane);
-    emit_obs(p.obs ? p.obs + env * 10 * A : nullptr, p.mask ? p.mask + env * A : nullptr, sR, sM, fc, g, lane,
-             reinterpret_cast<uint8_t*>(sTab));
+    emit_obs(p.obs ? p.obs + env * 10 * A : nullptr, p.mask ? p.mask + env * A : nullptr,
+             p.codes ? p.codes + env * A : nullptr, sR, sM, fc, g, lane, reinterpret_cast<uint8_t*>(sTab));
   }
   __syncthreads();
 }
@@ -1954,7 +1965,7 @@ __global__ __launch_bounds__(64 * EPW) void k_run(KParams p, RunParams r) {
     }
     if (p.obs || p.mask) {
       stage_rows(sR, sM, rev, mine, g, lane);
-      emit_obs(p.obs ? p.obs + slot * 10 * A : nullptr, p.mask ? p.mask + slot * A : nullptr, sR, sM, fc, g, lane,
+      emit_obs(p.obs ? p.obs + slot * 10 * A : nullptr, p.mask ? p.mask + slot * A : nullptr, nullptr, sR, sM, fc, g, lane,
                reinterpret_cast<uint8_t*>(sTab));
     }
     wave_sync();  // this step's LDS reads before the next step's placement / staging writes
@@ -2316,7 +2327,7 @@ void launch_step(const KParams& p, int epw, hipStream_t s, hipEvent_t ev0, hipEv
     // small boards: four per wave (k_step_packed); its float4 / dword stores need a
     // 16-B obs and 4-B mask base
     if (p.K >= 1 && p.K <= 16 && !(p.dbg_flags & (MS_DBG_ONE_BOARD_PER_WAVE | MS_DBG_FORCE_CHAIN_PLACEMENT)) &&
-        ((uintptr_t)p.obs & 15u) == 0 && ((uintptr_t)p.mask & 3u) == 0) {
+        ((uintptr_t)p.obs & 15u) == 0 && ((uintptr_t)p.mask & 3u) == 0 && !p.codes) {
       constexpr int WPG = 4;
       if (p.dbg_flags & MS_DBG_TWO_BOARDS_PER_WAVE) {
         const unsigned grid = (unsigned)((p.n + 2 * WPG - 1) / (2 * WPG));
@@ -2401,11 +2412,15 @@ int launch_late(const ms_handle* h, const KParams& p, const uint8_t* need, hipSt
 }
 
 int do_step(ms_handle* h, const void* actions, int i32, float* obs, uint8_t* mask, float* reward,
-            uint8_t* done, int32_t* step, int32_t* last_new, double* frac, int8_t* outcome, void* stream) {
+            uint8_t* done, int32_t* step, int32_t* last_new, double* frac, int8_t* outcome, void* stream,
+            uint8_t* codes = nullptr) {
   if (!h) return fail(MS_EINVAL, "ms_step: null handle");
   if (!actions) return fail(MS_EINVAL, "ms_step: null actions");
-  KParams p;
+  if (codes && ((h->H * h->W) & 3) == 0 && ((uintptr_t)codes & 3u) != 0)
+    return fail(MS_EINVAL, "ms_step_codes: codes must be 4-byte aligned");
+  KParams p = {};
   p.actions = actions;
+  p.codes = codes;
   p.obs = obs;
   p.mask = mask;
   p.reward = reward;
@@ -2646,6 +2661,11 @@ int ms_step(ms_handle* h, const int64_t* actions, float* obs, uint8_t* mask, flo
 int ms_step_i32(ms_handle* h, const int32_t* actions, float* obs, uint8_t* mask, float* reward, uint8_t* done,
                 int32_t* step, int32_t* last_new, double* revealed_frac, int8_t* outcome, void* stream) {
   return do_step(h, actions, 1, obs, mask, reward, done, step, last_new, revealed_frac, outcome, stream);
+}
+
+int ms_step_codes(ms_handle* h, const int64_t* actions, uint8_t* codes, uint8_t* mask, float* reward, uint8_t* done,
+                  int32_t* step, int32_t* last_new, double* revealed_frac, int8_t* outcome, void* stream) {
+  return do_step(h, actions, 0, nullptr, mask, reward, done, step, last_new, revealed_frac, outcome, stream, codes);
 }
 
 int ms_run_tape(ms_handle* h, uint64_t t0, int32_t T, int32_t mode, int32_t slots, int64_t* actions, float* obs,

@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # MSENV_LIB may point at libmsenv_diag.so (tools/diag_step.py); default is the product build
 LIB_PATH = os.environ.get("MSENV_LIB") or os.path.join(PKG_DIR, "libmsenv.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 MS_OUTCOME_NONE, MS_OUTCOME_WIN, MS_OUTCOME_LOSS = 0, 1, 2
 MS_TAPE_UNIFORM, MS_TAPE_SAFE_BIASED = 0, 1
@@ -47,6 +47,7 @@ SIGNATURES = {
     "ms_reset": [_vp, _vp, _vp, _vp],
     "ms_step": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ms_step_i32": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "ms_step_codes": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ms_labels": [_vp, _vp, _vp, _vp],
     "ms_snapshot": [_vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "ms_rng_state": [_vp, _vp, _vp],

@@ -274,8 +274,12 @@ class VecMinesweeper:
     def step(self, actions, out: Optional[Dict[str, torch.Tensor]] = None):
         a = self._as_actions(actions)
         n = self.num_envs
+        codes = out.get("codes") if out is not None else None
+        if codes is not None:  # the rollout buffer's u8 cell codes instead of the f32 obs (ms_step_codes)
+            assert codes.dtype == torch.uint8 and codes.is_contiguous() and codes.numel() == n * self.H * self.W
+            a = a.to(torch.int64)
         if out is not None:
-            obs, mask = out["obs"], out["action_mask"]
+            obs, mask = out.get("obs"), out["action_mask"]
             rewards, dones = out["rewards"], out["dones"]
         else:
             obs, mask = self._alloc_obs()
@@ -285,9 +289,12 @@ class VecMinesweeper:
         last_new = torch.empty(n, dtype=torch.int32, device=self.device)
         frac = torch.empty(n, dtype=torch.float64, device=self.device)
         outcome = torch.empty(n, dtype=torch.int8, device=self.device)
-        fn = self._lib.ms_step if a.dtype == torch.int64 else self._lib.ms_step_i32
+        if codes is not None:
+            fn, o = self._lib.ms_step_codes, codes
+        else:
+            fn, o = (self._lib.ms_step if a.dtype == torch.int64 else self._lib.ms_step_i32), obs
         with torch.cuda.device(self.device):
-            L.check(fn(self._h, L.ptr(a), L.ptr(obs), L.ptr(mask), L.ptr(rewards), L.ptr(dones),
+            L.check(fn(self._h, L.ptr(a), L.ptr(o), L.ptr(mask), L.ptr(rewards), L.ptr(dones),
                        L.ptr(step), L.ptr(last_new), L.ptr(frac), L.ptr(outcome), self._stream()))
         self._version += 1
         infos = _LazyInfos(step, last_new, frac, outcome, dones)

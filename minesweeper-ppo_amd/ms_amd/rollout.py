@@ -66,8 +66,8 @@ def collect_rollout(vec: VecMinesweeper, model: torch.nn.Module, steps: int, dev
     the reference's keys (train_rl.py:278-288), timed on the GPU with HIP events and resolved (one
     host sync) on first read (ms_amd.profiling.RolloutTimings); ``timing=False`` records no events.
     ``buffer`` may be passed back in to reuse its HBM (2.7 GB at N=4096, T=64; 67 MB with
-    ``obs_codes``: the buffer then holds u8 cell codes, the env's obs going through a
-    one-step scratch and ms_amd.fused.obs_encode)."""
+    ``obs_codes``: the buffer then holds u8 cell codes, which the env step writes directly
+    (ms_step_codes); only the reset obs and the last step's obs pass through f32)."""
     device = torch.device(device)
     need_aux = aux_mine_weight > 0 or aux_mine_calib_weight > 0
     N, H, W = vec.num_envs, vec.H, vec.W
@@ -86,7 +86,7 @@ def collect_rollout(vec: VecMinesweeper, model: torch.nn.Module, steps: int, dev
     s0 = buffer.slot(0)
     last_obs = torch.empty((N, OBS_CHANNELS, H, W), dtype=torch.float32, device=device)
     last_mask = torch.empty((N, H * W), dtype=torch.bool, device=device)
-    # codes mode: the env writes each step's f32 obs into last_obs, encoded into the buffer
+    # codes mode: the reset obs goes through last_obs (f32) and is encoded into slot 0
     vec.reset(out={"obs": last_obs if buffer.obs_codes else s0["obs"], "action_mask": s0["action_mask"]})
     if buffer.obs_codes:
         obs_encode(last_obs, s0["obs"])
@@ -108,16 +108,15 @@ def collect_rollout(vec: VecMinesweeper, model: torch.nn.Module, steps: int, dev
         tm.split("tensor_bridge")
         if t + 1 < steps:
             nxt = buffer.slot(t + 1)
-            out = {"obs": last_obs if buffer.obs_codes else nxt["obs"], "action_mask": nxt["action_mask"]}
+            # codes buffer: the env writes the next step's cell codes straight into it (ms_step_codes)
+            out = ({"codes": nxt["obs"], "action_mask": nxt["action_mask"]} if buffer.obs_codes else
+                   {"obs": nxt["obs"], "action_mask": nxt["action_mask"]})
         else:
             out = {"obs": last_obs, "action_mask": last_mask}
         out["rewards"], out["dones"] = s["rewards"], s["dones"]
         with prange("rollout/env_step"):
             vec.step(s["actions"], out=out)
         tm.split("env_step")
-        if buffer.obs_codes and t + 1 < steps:
-            obs_encode(last_obs, nxt["obs"])
-            tm.split("tensor_bridge")
     with prange("rollout/bootstrap"), _autocast(device, amp_dtype), \
             keyed_dropout(model, env_ids + steps * vec.num_envs_total, dseed, sample_counter + steps):
         _, last_values = model(last_obs)

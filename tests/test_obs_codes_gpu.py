@@ -57,6 +57,37 @@ def test_obs_codes_roundtrip(gpu, H, W, K, dt):
     assert torch.equal(c2, codes[5:])
 
 
+@pytest.mark.parametrize("H,W,K,late", [(16, 16, 40, False), (9, 9, 10, False), (30, 16, 99, False),
+                                        (5, 7, 3, False), (16, 16, 40, True), (9, 9, 10, True)])
+def test_step_codes_equals_encoded_obs(gpu, H, W, K, late):
+    """ms_step_codes (the env writing the buffer's cell codes itself) against ms_step + obs_encode
+    on twin handles: codes, mask, rewards, dones and the RNG states stay equal step for step,
+    auto-resets and late-start resets (the k_late emit) included."""
+    from ms_amd import EnvConfig, VecMinesweeper
+    from ms_amd.fused import obs_encode
+    N = 301
+    cfg = {"prob": 0.5, "min_hidden": 5, "max_hidden": H * W // 2} if late else None
+    vs = [VecMinesweeper(N, EnvConfig(H=H, W=W, mine_count=K), seed=5, device=gpu, late_start_cfg=cfg)
+          for _ in range(2)]
+    for v in vs:
+        v.reset()
+    for t in range(40):
+        a = vs[0].tape_actions(t, t % 2)
+        b0, r0, d0, _ = vs[0].step(a)
+        ref = torch.empty((N, H, W), dtype=torch.uint8, device=gpu)
+        obs_encode(b0["obs"].contiguous(), ref)
+        codes = torch.full((N, H, W), 77, dtype=torch.uint8, device=gpu)
+        out = {"codes": codes, "action_mask": torch.empty((N, H * W), dtype=torch.bool, device=gpu),
+               "rewards": torch.empty(N, dtype=torch.float32, device=gpu),
+               "dones": torch.empty(N, dtype=torch.bool, device=gpu)}
+        vs[1].step(a, out=out)
+        assert torch.equal(codes, ref), t
+        assert torch.equal(out["action_mask"], b0["action_mask"]) and torch.equal(out["rewards"], r0)
+        assert torch.equal(out["dones"], d0)
+    import numpy as np
+    assert np.array_equal(np.asarray(vs[0].rng_state()), np.asarray(vs[1].rng_state()))
+
+
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 def test_obs_to_nhwc_any_f32_input(gpu, dt):
     """The fused model's input conversion of an f32 obs is the cast of its values, whatever they

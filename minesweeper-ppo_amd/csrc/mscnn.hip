@@ -666,89 +666,95 @@ __global__ __launch_bounds__(512, 1) void k_conv_gn_fwd_ws(FwdParams<E> p) {
     }
   } else {
     // =============================== memory waves ===============================
-    const int mtid = threadIdx.x - 256;
+    const int mtid0 = threadIdx.x - 256;
     u32x4 xr[NXC];   // the next input tile but one, in flight
     u32x4 rq[NEC];   // the residual of the sample whose epilogue runs next
-    auto xload = [&](int n) {
-      const u32x4* xs = reinterpret_cast<const u32x4*>(p.x + (size_t)n * P * CIN);
-#pragma unroll
-      for (int k = 0; k < NXC; ++k) {
-        const int i = mtid + 256 * k;
-        if ((FULL && (k + 1) * 256 <= NPT * 128 * C8) || i < P * C8) xr[k] = xs[i];
-      }
-    };
-    auto xstore = [&](int region) {
-      E* sx = sReg + region * REG;
-#pragma unroll
-      for (int k = 0; k < NXC; ++k) {
-        const int i = mtid + 256 * k;
-        if ((FULL && (k + 1) * 256 <= NPT * 128 * C8) || i < P * C8) {
-          const int px = i / C8, c8 = i - px * C8;
-          *reinterpret_cast<u32x4*>(&sx[px * CINP + c8 * 8]) = xr[k];
-        }
-      }
-      if (mtid <= C8) *reinterpret_cast<u32x4*>(&sx[P * CINP + mtid * 8]) = u32x4{0u, 0u, 0u, 0u};  // zero row
-    };
-    auto rload = [&](int n) {
-      const u32x4* rs = reinterpret_cast<const u32x4*>(p.res + (size_t)n * P * COUT);
-#pragma unroll
-      for (int k = 0; k < NEC; ++k) {
-        const int c = mtid + 256 * k;
-        rq[k] = u32x4{0u, 0u, 0u, 0u};
-        if (FULL || c < P * (COUT / 8)) rq[k] = rs[c];
-      }
-    };
-    // epilogue segment j of sample n (its y in region rg): the chunks k = j + 3u share one
-    // channel octet cg, whose scale / shift / dropout scale are read once
-    auto epi = [&](int n, int rg, int j) {
-      const E* sY = sReg + rg * REG;
-      const float* co = sCoef + rg * 3 * COUT;
-      const int cg = (mtid % (COUT / 8) + 4 * j) % (COUT / 8);
-      float ca[8], cb[8], cd[8];
-#pragma unroll
-      for (int h4 = 0; h4 < 2; ++h4) {
-        const f32x4 a4 = *reinterpret_cast<const f32x4*>(&co[cg * 8 + 4 * h4]);
-        const f32x4 b4 = *reinterpret_cast<const f32x4*>(&co[COUT + cg * 8 + 4 * h4]);
-        const f32x4 d4 = *reinterpret_cast<const f32x4*>(&co[2 * COUT + cg * 8 + 4 * h4]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          ca[4 * h4 + e] = a4[e];
-          cb[4 * h4 + e] = b4[e];
-          cd[4 * h4 + e] = d4[e];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < EPS; ++u) {
-        const int k = j + 3 * u, c = mtid + 256 * k;
-        if (FULL || c < P * (COUT / 8)) {
-          const int px = c / (COUT / 8);
-          const size_t o = (size_t)n * P * COUT + (size_t)c * 8;
-          const u32x4 yv = *reinterpret_cast<const u32x4*>(&sY[px * YS + cg * 8]);
-          if (p.ysave) *reinterpret_cast<u32x4*>(&p.ysave[o]) = yv;
-          const E8 y8 = __builtin_bit_cast(E8, yv);
-          const E8 r8 = __builtin_bit_cast(E8, rq[k]);
-          E8 o8;
-          uint32_t mb = 0u;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float z = fmaxf((float)y8[e] * ca[e] + cb[e] + (float)r8[e], 0.f);
-            o8[e] = (E)(z * cd[e]);
-            mb |= ((float)o8[e] > 0.f ? 1u : 0u) << e;
-          }
-          *reinterpret_cast<u32x4*>(&p.out[o]) = __builtin_bit_cast(u32x4, o8);
-          if (p.rmask) p.rmask[(size_t)n * P * (COUT / 8) + c] = (uint8_t)mb;
-        }
-      }
-    };
 #pragma unroll
     for (int k = 0; k < NEC; ++k) rq[k] = u32x4{0u, 0u, 0u, 0u};
-    if (cnt > 0) {
-      xload((int)blockIdx.x);
-      xstore(0);
-      if (mtid <= C8) *reinterpret_cast<u32x4*>(&sReg[REG + P * CINP + mtid * 8]) = u32x4{0u, 0u, 0u, 0u};
-    }
-    if (cnt > 1) xload((int)blockIdx.x + G);
-    for (int it = 0; it <= cnt; ++it) {
+    for (int it = -1; it <= cnt; ++it) {
+      // loop-variant thread id: the per-chunk address math stays inside the loop (hoisted, the
+      // chunks' 64-bit addresses spill on boards with runtime guards)
+      const int mtid = mtid0 + opaque0();
+      auto xload = [&](int n) {
+        const u32x4* xs = reinterpret_cast<const u32x4*>(p.x + (size_t)n * P * CIN);
+  #pragma unroll
+        for (int k = 0; k < NXC; ++k) {
+          const int i = mtid + 256 * k;
+          if ((FULL && (k + 1) * 256 <= NPT * 128 * C8) || i < P * C8) xr[k] = xs[i];
+        }
+      };
+      auto xstore = [&](int region) {
+        E* sx = sReg + region * REG;
+  #pragma unroll
+        for (int k = 0; k < NXC; ++k) {
+          const int i = mtid + 256 * k;
+          if ((FULL && (k + 1) * 256 <= NPT * 128 * C8) || i < P * C8) {
+            const int px = i / C8, c8 = i - px * C8;
+            *reinterpret_cast<u32x4*>(&sx[px * CINP + c8 * 8]) = xr[k];
+          }
+        }
+        if (mtid <= C8) *reinterpret_cast<u32x4*>(&sx[P * CINP + mtid * 8]) = u32x4{0u, 0u, 0u, 0u};  // zero row
+      };
+      auto rload = [&](int n) {
+        const u32x4* rs = reinterpret_cast<const u32x4*>(p.res + (size_t)n * P * COUT);
+  #pragma unroll
+        for (int k = 0; k < NEC; ++k) {
+          const int c = mtid + 256 * k;
+          rq[k] = u32x4{0u, 0u, 0u, 0u};
+          if (FULL || c < P * (COUT / 8)) rq[k] = rs[c];
+        }
+      };
+      // epilogue segment j of sample n (its y in region rg): the chunks k = j + 3u share one
+      // channel octet cg, whose scale / shift / dropout scale are read once
+      auto epi = [&](int n, int rg, int j) {
+        const E* sY = sReg + rg * REG;
+        const float* co = sCoef + rg * 3 * COUT;
+        const int cg = (mtid % (COUT / 8) + 4 * j) % (COUT / 8);
+        float ca[8], cb[8], cd[8];
+  #pragma unroll
+        for (int h4 = 0; h4 < 2; ++h4) {
+          const f32x4 a4 = *reinterpret_cast<const f32x4*>(&co[cg * 8 + 4 * h4]);
+          const f32x4 b4 = *reinterpret_cast<const f32x4*>(&co[COUT + cg * 8 + 4 * h4]);
+          const f32x4 d4 = *reinterpret_cast<const f32x4*>(&co[2 * COUT + cg * 8 + 4 * h4]);
+  #pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            ca[4 * h4 + e] = a4[e];
+            cb[4 * h4 + e] = b4[e];
+            cd[4 * h4 + e] = d4[e];
+          }
+        }
+  #pragma unroll
+        for (int u = 0; u < EPS; ++u) {
+          const int k = j + 3 * u, c = mtid + 256 * k;
+          if (FULL || c < P * (COUT / 8)) {
+            const int px = c / (COUT / 8);
+            const size_t o = (size_t)n * P * COUT + (size_t)c * 8;
+            const u32x4 yv = *reinterpret_cast<const u32x4*>(&sY[px * YS + cg * 8]);
+            if (p.ysave) *reinterpret_cast<u32x4*>(&p.ysave[o]) = yv;
+            const E8 y8 = __builtin_bit_cast(E8, yv);
+            const E8 r8 = __builtin_bit_cast(E8, rq[k]);
+            E8 o8;
+            uint32_t mb = 0u;
+  #pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float z = fmaxf((float)y8[e] * ca[e] + cb[e] + (float)r8[e], 0.f);
+              o8[e] = (E)(z * cd[e]);
+              mb |= ((float)o8[e] > 0.f ? 1u : 0u) << e;
+            }
+            *reinterpret_cast<u32x4*>(&p.out[o]) = __builtin_bit_cast(u32x4, o8);
+            if (p.rmask) p.rmask[(size_t)n * P * (COUT / 8) + c] = (uint8_t)mb;
+          }
+        }
+      };
+      if (it < 0) {  // prologue: x(0) into region 0, both zero rows, x(1) in flight
+        if (cnt > 0) {
+          xload((int)blockIdx.x);
+          xstore(0);
+          if (mtid <= C8) *reinterpret_cast<u32x4*>(&sReg[REG + P * CINP + mtid * 8]) = u32x4{0u, 0u, 0u, 0u};
+        }
+        if (cnt > 1) xload((int)blockIdx.x + G);
+        continue;
+      }
       const int np = (int)blockIdx.x + (it - 1) * G;  // the sample whose epilogue runs now
       const bool ep = it >= 1;
       const int rg = (it + 1) & 1;                    // its y; then x(it+1) is staged there

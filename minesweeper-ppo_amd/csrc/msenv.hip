@@ -1715,7 +1715,7 @@ template <int H_, int W_>
 __device__ __forceinline__ void late_env(const KParams& p, Pcg& L, const LateCfg& lc, int64_t env,
                                          const uint64_t (&J)[4], uint64_t* sR, uint64_t* sM, uint32_t* sTab,
                                          const Geo<H_, W_>& g, int lane) {
-  const int H = g.H, W = g.W, A = g.A(), NW = g.NW();
+  const int H = g.H, A = g.A(), NW = g.NW();
   const uint64_t rowmask = g.rowmask();
   const int safe_total = A - p.K;
   EnvMeta* mp = p.meta + env;
@@ -1753,24 +1753,47 @@ __device__ __forceinline__ void late_env(const KParams& p, Pcg& L, const LateCfg
       target = target < safe_total ? target : safe_total;
       target = target > 1 ? target : 1;
       int revealed = (int)tr;
+      // The extra clicks hit safe unrevealed cells of a placed board (the candidates are
+      // ~mine & ~revealed, flags are never set), so each is MinesweeperEnv.step's reveal branch
+      // alone: the candidates number safe_total - revealed (no count reduction), a cell with
+      // adjacent mines reveals just itself (no flood-fill fixpoint), and the step ends the
+      // episode only by a win. The mines are fixed now: their zero-cell map is built once.
+      const uint64_t Um = wave_shr1(mine) | wave_shl1(mine);
+      const uint64_t zero = ~(Um | (Um << 1) | (Um >> 1) | (mine << 1) | (mine >> 1)) & rowmask;
       for (int k = 0; k < lc.max_extra_steps; ++k) {
         if (safe_total - revealed <= target) {
           success = true;
           break;
         }
+        const uint32_t cnt = (uint32_t)(safe_total - revealed);
         const uint64_t cand = ~mine & ~rev & (lane < H ? rowmask : 0ull);
         const uint32_t pc = (uint32_t)__popcll(cand);
-        const uint32_t cnt = wave_sum(pc);
-        if (cnt == 0) break;
         const uint32_t kk = pcg_bounded(L, cnt - 1u);  // rng.choice(flatnonzero(...)) (row-major)
         const uint32_t before = wave_excl_scan(pc);
         const bool mine_lane = kk >= before && kk < before + pc;
         const uint64_t who = __ballot(mine_lane);
         const int src = __ffsll((unsigned long long)who) - 1;
         const int col = (int)readlane32((uint32_t)(mine_lane ? select_bit(cand, kk - before) : 0), src);
-        board_click(rng, mine, rev, fc, src * W + col, p, J, sTab, sR, g, lane, done, oc, nw, tr, mc);
+        if (((readlane64(zero, src) >> col) & 1ull) == 0ull) {
+          if (lane == src) rev |= 1ull << col;
+          revealed += 1;
+        } else {  // flood_fill_reveal (env_numba.py:17-77) from a zero cell, as board_click
+          const uint64_t allow = ~mine & ~rev & (lane < H ? rowmask : 0ull);
+          uint64_t Fr = (lane == src) ? (1ull << col) : 0ull;
+          while (true) {
+            const uint64_t S = Fr & zero;
+            const uint64_t Dh = S | (S << 1) | (S >> 1);
+            const uint64_t Dv = Dh | wave_shr1(Dh) | wave_shl1(Dh);
+            const uint64_t Fn = Fr | (Dv & allow);
+            const bool changed = __ballot(Fn != Fr) != 0ull;
+            Fr = Fn;
+            if (!changed) break;
+          }
+          rev |= Fr;
+          revealed += (int)wave_sum((uint32_t)__popcll(Fr));
+        }
         step_count += 1;
-        revealed = (int)tr;
+        done = revealed >= safe_total;  // a win (env.py:133-140)
         if (done) break;
       }
       if (!success && !done && safe_total - revealed <= target) success = true;
@@ -1827,9 +1850,15 @@ __global__ __launch_bounds__(64) void k_late(KParams p, Pcg* lstate, LateCfg lc,
   L.uinteger = lstate->uinteger;
   uint64_t J[4];
   load_jump(p.jump, lane, J);
-  for (int64_t env = 0; env < p.n; ++env) {
-    if (need && !need[env]) continue;
-    late_env(p, L, lc, env, J, sR, sM, sTab, g, lane);
+  // the flags of 64 envs per load and ballot (one dependent scalar load per env cost ~0.5 us each)
+  for (int64_t base = 0; base < p.n; base += kWave) {
+    const int64_t e = base + lane;
+    uint64_t todo = __ballot(e < p.n && (!need || need[e]));
+    while (todo) {
+      const int l = __ffsll((unsigned long long)todo) - 1;
+      todo &= todo - 1ull;
+      late_env(p, L, lc, base + l, J, sR, sM, sTab, g, lane);
+    }
   }
   if (lane == 0) {
     lstate->hi = L.hi;

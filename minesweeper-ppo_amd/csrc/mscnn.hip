@@ -436,6 +436,37 @@ __host__ __device__ inline size_t ws_lds_bytes(int P) {
   return (size_t)2 * ws_region_elems<CIN>(P) * 2 + (size_t)2 * COUT * cinp<CIN>() * 2 + (size_t)WS_FLOATS * 4;
 }
 
+// MC_DIAG builds: per segment (the stretch after each of the 11 barriers) the s_memtime ticks a
+// wave spent working and then waiting at the next barrier, for conv wave 0 and memory wave 4:
+// diag[(workgroup * 2 + role) * 24 + k] = work of segment k, [.. + 12 + k] = wait before barrier k+1.
+#ifdef MC_DIAG
+#define WS_DIAG_DECL                                  \
+  unsigned long long dwork[11], dwait[11];             \
+  for (int k_ = 0; k_ < 11; ++k_) dwork[k_] = dwait[k_] = 0ull; \
+  unsigned long long tprev = __builtin_amdgcn_s_memtime()
+#define WS_BAR(seg)                                          \
+  do {                                                       \
+    const unsigned long long t0_ = __builtin_amdgcn_s_memtime(); \
+    lds_barrier();                                           \
+    const unsigned long long t1_ = __builtin_amdgcn_s_memtime(); \
+    dwork[(seg)] += t0_ - tprev;                             \
+    dwait[(seg)] += t1_ - t0_;                               \
+    tprev = t1_;                                             \
+  } while (0)
+#define WS_DIAG_OUT(role)                                                                   \
+  do {                                                                                      \
+    if (p.diag && (threadIdx.x & 255) == 0)                                                 \
+      for (int k_ = 0; k_ < 11; ++k_) {                                                     \
+        p.diag[((size_t)blockIdx.x * 2 + (role)) * 24 + k_] = dwork[k_];                    \
+        p.diag[((size_t)blockIdx.x * 2 + (role)) * 24 + 12 + k_] = dwait[k_];               \
+      }                                                                                     \
+  } while (0)
+#else
+#define WS_DIAG_DECL do { } while (0)
+#define WS_BAR(seg) lds_barrier()
+#define WS_DIAG_OUT(role) do { } while (0)
+#endif
+
 template <typename E, int CIN, int NPT, bool FULL>
 __global__ __launch_bounds__(512, 1) void k_conv_gn_fwd_ws(FwdParams<E> p) {
   typedef typename EV<E>::v8 E8;
@@ -463,6 +494,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_gn_fwd_ws(FwdParams<E> p) {
     // =============================== conv waves ===============================
     const int ctid = threadIdx.x;
     const int l32 = lane & 31, hh = lane >> 5;
+    WS_DIAG_DECL;
     for (int i = ctid; i < COUT; i += 256) {
       sBias[i] = p.bias[i];
       sGB[i] = p.gamma[i];
@@ -507,7 +539,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_gn_fwd_ws(FwdParams<E> p) {
       const int n = (int)blockIdx.x + it * G;
       const E* sX = sReg + (it & 1) * REG;
       float dmv = 1.f;
-      lds_barrier();  // A: x(it) staged, tap 0 in its slot
+      WS_BAR(10);  // A: x(it) staged, tap 0 in its slot
       f32x16 acc[NPT][3];
       if (conv) {
         if (p.dmask && ctid < COUT) dmv = p.dmask[(size_t)n * COUT + ctid];  // used after the taps
@@ -523,7 +555,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_gn_fwd_ws(FwdParams<E> p) {
           }
       }
       for (int tap = 0; tap < 9; ++tap) {
-        if (tap) lds_barrier();  // T_tap: the ring slot of this tap is written, the other one free
+        if (tap) WS_BAR(tap - 1);  // T_tap: the ring slot of this tap is written, the other one free
         if (!conv) continue;
         const int g = it * 9 + tap;
         if (g + 1 < total) wstore((g + 1) & 1);  // registers hold tap (g+1) mod 9
@@ -580,7 +612,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_gn_fwd_ws(FwdParams<E> p) {
             if (lane == 0) sRed[wave * NGRP + 2 * ct + hf] = s;
           }
       }
-      lds_barrier();  // S1: every conv wave's reads of x(it) done; pass-1 sums posted
+      WS_BAR(8);  // S1: every conv wave's reads of x(it) done; pass-1 sums posted
       if (conv) {
 #pragma unroll
         for (int g = 0; g < NGRP; ++g) {
@@ -627,7 +659,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_gn_fwd_ws(FwdParams<E> p) {
             if (lane == 0) sRed[WAVES * NGRP + wave * NGRP + 2 * ct + hf] = s;
           }
       }
-      lds_barrier();  // S2: pass-2 sums posted
+      WS_BAR(9);  // S2: pass-2 sums posted
       if (conv) {
 #pragma unroll
         for (int g = 0; g < NGRP; ++g) {
@@ -664,9 +696,11 @@ __global__ __launch_bounds__(512, 1) void k_conv_gn_fwd_ws(FwdParams<E> p) {
         }
       }
     }
+    WS_DIAG_OUT(0);
   } else {
     // =============================== memory waves ===============================
     const int mtid0 = threadIdx.x - 256;
+    WS_DIAG_DECL;
     u32x4 xr[NXC];   // the next input tile but one, in flight
     u32x4 rq[NEC];   // the residual of the sample whose epilogue runs next
 #pragma unroll
@@ -758,24 +792,25 @@ __global__ __launch_bounds__(512, 1) void k_conv_gn_fwd_ws(FwdParams<E> p) {
       const int np = (int)blockIdx.x + (it - 1) * G;  // the sample whose epilogue runs now
       const bool ep = it >= 1;
       const int rg = (it + 1) & 1;                    // its y; then x(it+1) is staged there
-      lds_barrier();  // A
+      WS_BAR(10);  // A
       if (ep) epi(np, rg, 0);
-      lds_barrier();  // T1
+      WS_BAR(0);  // T1
       if (ep) epi(np, rg, 1);
-      lds_barrier();  // T2
+      WS_BAR(1);  // T2
       if (ep) epi(np, rg, 2);
-      lds_barrier();  // T3: every memory wave's reads of y(it-1) done
-      lds_barrier();  // T4
+      WS_BAR(2);  // T3: every memory wave's reads of y(it-1) done
+      WS_BAR(3);  // T4
       if (it + 1 < cnt) xstore(rg);
-      lds_barrier();  // T5
+      WS_BAR(4);  // T5
       if (it + 2 < cnt) xload((int)blockIdx.x + (it + 2) * G);
       if (it < cnt && p.res) rload((int)blockIdx.x + it * G);
-      lds_barrier();  // T6
-      lds_barrier();  // T7
-      lds_barrier();  // T8
-      lds_barrier();  // S1
-      lds_barrier();  // S2
+      WS_BAR(5);  // T6
+      WS_BAR(6);  // T7
+      WS_BAR(7);  // T8
+      WS_BAR(8);  // S1
+      WS_BAR(9);  // S2
     }
+    WS_DIAG_OUT(1);
   }
 }
 

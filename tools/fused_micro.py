@@ -48,11 +48,12 @@ for var in (int(v) for v in args.variants.split(",")):
         f1 = t(lambda: conv_gn_fwd(x, wt, b, g, be, H, W, res=res, want_mask=args.mask), args.iters)
         print(f"[variant {var}] fused conv+GN+res+ReLU  n={n} {H}x{W}: {f1 * 1e3:.3f} ms  "
               f"{flop / f1 / 1e12:.0f} TFLOP/s(conv)", flush=True)
-        if args.bwd:
-            out, y, st = conv_gn_fwd(x, wt, b, g, be, H, W, res=res)
+        if args.bwd:  # the trainer's path: the forward's ReLU bitmask, the skip addend, dz kept
+            out, y, st, rm = conv_gn_fwd(x, wt, b, g, be, H, W, res=res, want_mask=True)
             dout = torch.randn_like(out)
             wT = prep_weight_t(w)
-            fb = t(lambda: conv_gn_bwd(dout, out, y, st, g, x, H, W, wT=wT, addend=res, want_dz=True), args.iters)
+            fb = t(lambda: conv_gn_bwd(dout, None, y, st, g, x, H, W, wT=wT, addend=res, want_dz=True, rmask=rm),
+                   args.iters)
             print(f"[variant {var}] fused bwd (GN-bwd + dgrad + wgrad) n={n} {H}x{W}: {fb * 1e3:.3f} ms  "
                   f"{2 * flop / fb / 1e12:.0f} TFLOP/s", flush=True)
 if args.no_torch:

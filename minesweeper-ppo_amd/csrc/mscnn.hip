@@ -424,7 +424,7 @@ int launch_fwd(const FwdParams<E>& p, hipStream_t s) {
 // iteration (loop top, 8 between taps, 2 for the statistics): the memory waves' work is laid
 // over the first taps' segments, their loads issued six segments before use.
 constexpr int YS = COUT + 8;  // y staging row stride (elements): 2-way ds_write_b64, conflict-free b128 reads
-constexpr int WS_FLOATS = COUT + 2 * COUT + 2 * 3 * COUT + 2 * WAVES * NGRP;
+constexpr int WS_FLOATS = COUT + 2 * COUT + 2 * 3 * COUT + 2 * WAVES * NGRP + 4;  // + 2 group-barrier counters
 
 template <int CIN>
 __host__ __device__ inline int ws_region_elems(int P) {
@@ -467,7 +467,9 @@ __host__ __device__ inline size_t ws_lds_bytes(int P) {
 #define WS_DIAG_OUT(role) do { } while (0)
 #endif
 
-template <typename E, int CIN, int NPT, bool FULL>
+// GB: the roles sync inside an iteration with their own LDS-counter barriers (grp_bar) and meet
+// at one s_barrier per iteration; without GB every wave passes all 11 s_barriers.
+template <typename E, int CIN, int NPT, bool FULL, bool GB>
 __global__ __launch_bounds__(512, 1) void k_conv_gn_fwd_ws(FwdParams<E> p) {
   typedef typename EV<E>::v8 E8;
   typedef typename EV<E>::v4 E4;
@@ -485,6 +487,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_gn_fwd_ws(FwdParams<E> p) {
   float* sGB = sBias + COUT;           // gamma | beta
   float* sCoef = sGB + 2 * COUT;       // [2][scale | shift | dropout scale][COUT]
   float* sRed = sCoef + 6 * COUT;      // [2 passes][WAVES][NGRP]
+  unsigned* sCnt = reinterpret_cast<unsigned*>(sRed + 2 * WAVES * NGRP);  // conv | memory grp_bar counters
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int lane = threadIdx.x & 63;
   const int G = gridDim.x;
@@ -500,6 +503,13 @@ __global__ __launch_bounds__(512, 1) void k_conv_gn_fwd_ws(FwdParams<E> p) {
       sGB[i] = p.gamma[i];
       sGB[COUT + i] = p.beta[i];
     }
+    if (ctid < 2) sCnt[ctid] = 0u;
+    unsigned gbt = 0u;  // GB: this role's barriers passed x 4
+#define CONV_BAR(seg)                      \
+  do {                                     \
+    if (GB) grp_bar(&sCnt[0], gbt += 4u, lane); \
+    else WS_BAR(seg);                      \
+  } while (0)
     u32x4 wr[NWC];
     auto wload = [&](int tap) {
       const u32x4* ws = reinterpret_cast<const u32x4*>(p.wt + (size_t)tap * COUT * CIN);
@@ -555,7 +565,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_gn_fwd_ws(FwdParams<E> p) {
           }
       }
       for (int tap = 0; tap < 9; ++tap) {
-        if (tap) WS_BAR(tap - 1);  // T_tap: the ring slot of this tap is written, the other one free
+        if (tap) CONV_BAR(tap - 1);  // T_tap: the ring slot of this tap is written, the other one free
         if (!conv) continue;
         const int g = it * 9 + tap;
         if (g + 1 < total) wstore((g + 1) & 1);  // registers hold tap (g+1) mod 9
@@ -612,7 +622,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_gn_fwd_ws(FwdParams<E> p) {
             if (lane == 0) sRed[wave * NGRP + 2 * ct + hf] = s;
           }
       }
-      WS_BAR(8);  // S1: every conv wave's reads of x(it) done; pass-1 sums posted
+      CONV_BAR(8);  // S1: every conv wave's reads of x(it) done; pass-1 sums posted
       if (conv) {
 #pragma unroll
         for (int g = 0; g < NGRP; ++g) {
@@ -659,7 +669,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_gn_fwd_ws(FwdParams<E> p) {
             if (lane == 0) sRed[WAVES * NGRP + wave * NGRP + 2 * ct + hf] = s;
           }
       }
-      WS_BAR(9);  // S2: pass-2 sums posted
+      CONV_BAR(9);  // S2: pass-2 sums posted
       if (conv) {
 #pragma unroll
         for (int g = 0; g < NGRP; ++g) {
@@ -697,9 +707,11 @@ __global__ __launch_bounds__(512, 1) void k_conv_gn_fwd_ws(FwdParams<E> p) {
       }
     }
     WS_DIAG_OUT(0);
+#undef CONV_BAR
   } else {
     // =============================== memory waves ===============================
     const int mtid0 = threadIdx.x - 256;
+    unsigned gbt = 0u;
     WS_DIAG_DECL;
     u32x4 xr[NXC];   // the next input tile but one, in flight
     u32x4 rq[NEC];   // the residual of the sample whose epilogue runs next
@@ -792,6 +804,19 @@ __global__ __launch_bounds__(512, 1) void k_conv_gn_fwd_ws(FwdParams<E> p) {
       const int np = (int)blockIdx.x + (it - 1) * G;  // the sample whose epilogue runs now
       const bool ep = it >= 1;
       const int rg = (it + 1) & 1;                    // its y; then x(it+1) is staged there
+      if (GB) {  // one s_barrier per iteration; the memory waves' own hand-off by grp_bar
+        WS_BAR(10);  // A: y(it-1) and its coefficients posted, x(it) read by nobody yet
+        if (ep) {
+          epi(np, rg, 0);
+          epi(np, rg, 1);
+          epi(np, rg, 2);
+        }
+        grp_bar(&sCnt[1], gbt += 4u, lane);  // every memory wave's reads of y(it-1) done
+        if (it + 1 < cnt) xstore(rg);
+        if (it + 2 < cnt) xload((int)blockIdx.x + (it + 2) * G);
+        if (it < cnt && p.res) rload((int)blockIdx.x + it * G);
+        continue;
+      }
       WS_BAR(10);  // A
       if (ep) epi(np, rg, 0);
       WS_BAR(0);  // T1
@@ -814,18 +839,18 @@ __global__ __launch_bounds__(512, 1) void k_conv_gn_fwd_ws(FwdParams<E> p) {
   }
 }
 
-template <typename E, int CIN, int NPT, bool FULL>
-int launch_fwd_ws(const FwdParams<E>& p, hipStream_t s) {
+template <typename E, int CIN, int NPT, bool FULL, bool GB>
+int launch_fwd_ws_t(const FwdParams<E>& p, hipStream_t s) {
   const size_t lds = ws_lds_bytes<CIN>(p.H * p.W);
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k_conv_gn_fwd_ws<E, CIN, NPT, FULL>,
+    (void)hipFuncSetAttribute((const void*)k_conv_gn_fwd_ws<E, CIN, NPT, FULL, GB>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   const int cap = num_cus();
   const int grid = p.N < cap ? p.N : cap;
-  hipLaunchKernelGGL((k_conv_gn_fwd_ws<E, CIN, NPT, FULL>), dim3(grid), dim3(512), lds, s, p);
+  hipLaunchKernelGGL((k_conv_gn_fwd_ws<E, CIN, NPT, FULL, GB>), dim3(grid), dim3(512), lds, s, p);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     snprintf(g_err, sizeof g_err, "mc_conv_gn_fwd launch: %s", hipGetErrorString(e));
@@ -834,12 +859,18 @@ int launch_fwd_ws(const FwdParams<E>& p, hipStream_t s) {
   return MS_OK;
 }
 
+template <typename E, int CIN, int NPT, bool FULL>
+int launch_fwd_ws(const FwdParams<E>& p, hipStream_t s) {
+  return g_variant[MCV_FWD] == 3 ? launch_fwd_ws_t<E, CIN, NPT, FULL, true>(p, s)
+                                 : launch_fwd_ws_t<E, CIN, NPT, FULL, false>(p, s);
+}
+
 template <typename E, int CIN>
 int dispatch_fwd(const FwdParams<E>& p, hipStream_t s) {
   const int P = p.H * p.W;
   const int tiles = (P + 31) / 32;
   const int npt = (tiles + WAVES - 1) / WAVES;
-  if (P <= 256 && g_variant[MCV_FWD] != 1) {
+  if (P <= 256 && g_variant[MCV_FWD] >= 2) {  // measured slower than the per-sample kernel so far
     if (P == 256) return launch_fwd_ws<E, CIN, 2, true>(p, s);
     if (P > 128) return launch_fwd_ws<E, CIN, 2, false>(p, s);
     return launch_fwd_ws<E, CIN, 1, false>(p, s);
@@ -959,7 +990,7 @@ extern "C" {
 const char* mc_last_error(void) { return g_err; }
 
 int mc_set_variant(int32_t kernel, int32_t variant) {
-  if (kernel < 0 || kernel >= MCV_COUNT || variant < 0 || variant > 2) {
+  if (kernel < 0 || kernel >= MCV_COUNT || variant < 0 || variant > 3) {
     snprintf(g_err, sizeof g_err, "mc_set_variant: bad kernel %d / variant %d", kernel, variant);
     return MS_EINVAL;
   }

@@ -377,10 +377,12 @@ constexpr int WSB_FOLD = 11;  // the 21 pixel groups' channel sums folded into 1
 
 __host__ __device__ inline size_t wsb_lds_bytes(int P) {
   return (size_t)2 * dtile_bytes(P) + (size_t)2 * COUT * DCP * 2 + (size_t)WSB_FOLD * 3 * COUT * 4 +
-         (size_t)5 * COUT * 4;
+         (size_t)5 * COUT * 4 + 16;  // + the grp_bar counters
 }
 
-template <typename E, int NPT, bool FULL>
+// GB: one s_barrier per iteration (the roles' hand-off), the rest of each role's syncs by its own
+// LDS-counter barrier (grp_bar); without GB every wave passes all 10 s_barriers.
+template <typename E, int NPT, bool FULL, bool GB>
 __global__ __launch_bounds__(512, 1) void k_bwd_data_ws(BwdDataParams<E> p) {
   typedef typename EV<E>::v8 E8;
   typedef typename EV<E>::v4 E4;
@@ -395,6 +397,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_data_ws(BwdDataParams<E> p) {
   float* sRed = reinterpret_cast<float*>(sRing + 2 * COUT * DCP);        // [WSB_FOLD][3][COUT]
   float* sTmp = sRed + WSB_FOLD * 3 * COUT;                              // [2][COUT]
   float* sCo = sTmp + 2 * COUT;                                          // [3][COUT]
+  unsigned* sCnt = reinterpret_cast<unsigned*>(sCo + 3 * COUT);          // dgrad | memory grp_bar counters
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int lane = threadIdx.x & 63;
   const int G = gridDim.x;
@@ -426,6 +429,8 @@ __global__ __launch_bounds__(512, 1) void k_bwd_data_ws(BwdDataParams<E> p) {
     wload(0);
     wstore(0);
     wload(1);
+    if (ctid < 2) sCnt[ctid] = 0u;
+    unsigned gbt = 0u;
     int qr[NPT], qc[NPT];
     bool qv[NPT];
 #pragma unroll
@@ -448,7 +453,10 @@ __global__ __launch_bounds__(512, 1) void k_bwd_data_ws(BwdDataParams<E> p) {
 #pragma unroll
           for (int i = 0; i < 16; ++i) acc[t][ct][i] = 0.f;
       for (int tap = 0; tap < 9; ++tap) {
-        if (tap) lds_barrier();  // T_tap
+        if (tap) {  // T_tap
+          if (GB) grp_bar(&sCnt[0], gbt += 4u, lane);
+          else lds_barrier();
+        }
         if (!conv) continue;
         const int g = it * 9 + tap;
         if (g + 1 < total) wstore((g + 1) & 1);
@@ -485,7 +493,8 @@ __global__ __launch_bounds__(512, 1) void k_bwd_data_ws(BwdDataParams<E> p) {
           __builtin_amdgcn_sched_group_barrier(0x008, 3 * NPT, 0);
         }
       }
-      lds_barrier();  // X1: every dgrad wave's reads of dy(it) done
+      if (GB) grp_bar(&sCnt[0], gbt += 4u, lane);  // X1: every dgrad wave's reads of dy(it) done
+      else lds_barrier();
       if (conv) {
 #pragma unroll
         for (int t = 0; t < NPT; ++t) {
@@ -508,6 +517,12 @@ __global__ __launch_bounds__(512, 1) void k_bwd_data_ws(BwdDataParams<E> p) {
     // =============================== memory waves ===============================
     const int mtid = threadIdx.x - 256;
     const float inv_cnt = 1.0f / (16.0f * (float)P);
+    unsigned gbt = 0u;
+#define MEM_BAR()                                  \
+  do {                                             \
+    if (GB) grp_bar(&sCnt[1], gbt += 4u, lane);    \
+    else lds_barrier();                            \
+  } while (0)
     float gam = 0.f, acc_g = 0.f, acc_b = 0.f, acc_bias = 0.f;  // mtid < 96: channel mtid
     if (mtid < COUT) gam = p.gamma[mtid];
     if (mtid < DCP / 8) {
@@ -591,8 +606,8 @@ __global__ __launch_bounds__(512, 1) void k_bwd_data_ws(BwdDataParams<E> p) {
       // sample f's pass-1 inputs, issued once the addend registers are free
       asm volatile("" ::: "memory");
       if (pf) gload((int)nf, dv, yr, mv, dm, smean, srstd, cmean, crstd);
-      lds_barrier();  // T1: dx(e) read; the region takes dz(f)
-      lds_barrier();  // T2
+      MEM_BAR();  // T1: dx(e) read; the region takes dz(f)
+      if (!GB) lds_barrier();  // T2
       if (pf && gact) {  // ---- pass 1: dz and the channel sums ----
 #pragma unroll
         for (int j = 0; j < 8; ++j) s1[j] = s2[j] = s3[j] = 0.f;
@@ -629,7 +644,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_data_ws(BwdDataParams<E> p) {
       // these loads above pass 1, where dout, y and the addend would all be live)
       asm volatile("" ::: "memory");
       if (it >= 0 && it < cnt) aload((int)blockIdx.x + it * G);
-      lds_barrier();  // T3
+      MEM_BAR();  // T3
       if (pf && gact && pg >= WSB_FOLD) {
         const int q = pg - WSB_FOLD;
 #pragma unroll
@@ -639,7 +654,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_data_ws(BwdDataParams<E> p) {
           sRed[(q * 3 + 2) * COUT + c8 * 8 + j] += s3[j];
         }
       }
-      lds_barrier();  // T4
+      MEM_BAR();  // T4
       if (pf && mtid < COUT) {
         float S2 = 0.f;
         S1 = S3 = 0.f;
@@ -653,7 +668,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_data_ws(BwdDataParams<E> p) {
         acc_g += S2;
         acc_b += S1;
       }
-      lds_barrier();  // T5
+      MEM_BAR();  // T5
       if (pf && mtid < COUT) {
         const int g0 = (mtid >> 4) * 16;
         float m1 = 0.f, m2 = 0.f;
@@ -668,7 +683,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_data_ws(BwdDataParams<E> p) {
         sCo[2 * COUT + mtid] = crstd * (crstd * m2 * cmean - m1);
         acc_bias += crstd * (gam * S1 - (float)P * m1 - m2 * S3);
       }
-      lds_barrier();  // T6
+      MEM_BAR();  // T6
       if (pf && gact) {  // ---- pass 2: dy (GroupNorm backward) -> LDS + HBM ----
         float A[8];
 #pragma unroll
@@ -692,11 +707,14 @@ __global__ __launch_bounds__(512, 1) void k_bwd_data_ws(BwdDataParams<E> p) {
           }
         }
       }
-      lds_barrier();  // T7
-      lds_barrier();  // T8
-      lds_barrier();  // X1
+      if (!GB) {
+        lds_barrier();  // T7
+        lds_barrier();  // T8
+        lds_barrier();  // X1
+      }
     }
 #undef WSB_GLOAD_VARS
+#undef MEM_BAR
     if (mtid < COUT) {
       p.part[((size_t)blockIdx.x * 3 + 0) * COUT + mtid] = acc_g;
       p.part[((size_t)blockIdx.x * 3 + 1) * COUT + mtid] = acc_b;
@@ -963,21 +981,26 @@ void launch_bwd_data(const BwdDataParams<E>& p, int grid, size_t lds, hipStream_
   else launch_bwd_data_t<E, NPT, DGRAD, NCH, false>(p, grid, lds, s);
 }
 
-template <typename E, int NPT, bool FULL>
-void launch_bwd_data_ws(const BwdDataParams<E>& p, int grid, hipStream_t s) {
+template <typename E, int NPT, bool FULL, bool GB>
+void launch_bwd_data_ws_t(const BwdDataParams<E>& p, int grid, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    set_lds_attr(k_bwd_data_ws<E, NPT, FULL>);
+    set_lds_attr(k_bwd_data_ws<E, NPT, FULL, GB>);
     attr = true;
   }
-  hipLaunchKernelGGL((k_bwd_data_ws<E, NPT, FULL>), dim3(grid), dim3(512), wsb_lds_bytes(p.H * p.W), s, p);
+  hipLaunchKernelGGL((k_bwd_data_ws<E, NPT, FULL, GB>), dim3(grid), dim3(512), wsb_lds_bytes(p.H * p.W), s, p);
+}
+template <typename E, int NPT, bool FULL>
+void launch_bwd_data_ws(const BwdDataParams<E>& p, int grid, hipStream_t s) {
+  if (g_variant[MCV_BWD] == 3) launch_bwd_data_ws_t<E, NPT, FULL, true>(p, grid, s);
+  else launch_bwd_data_ws_t<E, NPT, FULL, false>(p, grid, s);
 }
 
 // grid: in, the per-sample kernel's grid; out, the workgroups launched (= partial rows in p.part)
 template <typename E, bool DGRAD>
 int dispatch_bwd_data(const BwdDataParams<E>& p, int& grid, hipStream_t s) {
   const int P = p.H * p.W;
-  if (DGRAD && P <= 256 && p.rmask && g_variant[MCV_BWD] != 1) {
+  if (DGRAD && P <= 256 && p.rmask && g_variant[MCV_BWD] >= 2) {  // opt-in until measured faster
     const int ncu = num_cus();
     grid = p.N < ncu ? p.N : ncu;
     if (P == 256) launch_bwd_data_ws<E, 2, true>(p, grid, s);

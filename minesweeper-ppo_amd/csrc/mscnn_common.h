@@ -99,6 +99,16 @@ __device__ __forceinline__ float wave_sum(float v) {
   return (readlane_f(v, 15) + readlane_f(v, 31)) + (readlane_f(v, 47) + readlane_f(v, 63));
 }
 
+// Barrier among the 4 waves of one role of a wave-specialised workgroup, through a monotonic LDS
+// counter (s_barrier would hold the other role's waves too): each wave finishes its LDS work,
+// adds 1, and waits until the counter reaches target = 4 * (barriers passed so far).
+__device__ __forceinline__ void grp_bar(unsigned* cnt, unsigned target, int lane) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
+  asm volatile("" ::: "memory");
+}
+
 // Kernel variants (msenv_debug.h mc_set_variant): 0 = the dispatcher's choice.
 enum { MCV_FWD = 0, MCV_BWD = 1, MCV_COUNT = 2 };
 extern int g_variant[MCV_COUNT];

@@ -45,13 +45,13 @@ PROD = [pytest.param(16, 16, 96, 32768, id="c2-16x16-32768"), pytest.param(16, 1
                                        (16, 30, 96, 9), (5, 7, 16, 3)] + PROD)
 @pytest.mark.parametrize("with_res", [False, True])
 @pytest.mark.parametrize("dt", DT)
-@pytest.mark.parametrize("variant", [0, 1], ids=["dispatch", "per-sample"])
+@pytest.mark.parametrize("variant", [0, 2, 3], ids=["dispatch", "ws-sbarrier", "ws-grpbar"])
 def test_conv_gn_fwd_matches_torch(gpu, H, W, cin, n, with_res, dt, variant):
     """The fused forward (conv + bias + GroupNorm + affine [+ residual] + ReLU [+ dropout
-    scale]) and its ReLU bitmask vs a torch fp32 reference of the same op; for boards of
-    P <= 256 the dispatcher runs the wave-specialised kernel, variant 1 the per-sample one."""
+    scale]) and its ReLU bitmask vs a torch fp32 reference of the same op, on the dispatcher's
+    kernel and on both wave-specialised forms (P <= 256)."""
     from ms_amd.fused import VARIANT_FWD, kernel_variant
-    if variant == 1 and H * W > 256:
+    if variant >= 2 and H * W > 256:
         pytest.skip("P > 256 runs the per-sample kernel either way")
     with kernel_variant(VARIANT_FWD, variant):
         _fwd_case(gpu, H, W, cin, n, with_res, dt)
@@ -82,7 +82,8 @@ def _fwd_case(gpu, H, W, cin, n, with_res, dt):
 @pytest.mark.parametrize("H,W,cin,n", [(16, 16, 96, 2000), (16, 16, 16, 700), (9, 9, 96, 900), (12, 12, 96, 300),
                                        (5, 7, 16, 5)])
 @pytest.mark.parametrize("dt", DT)
-def test_fwd_wave_specialised_equals_per_sample(gpu, H, W, cin, n, dt):
+@pytest.mark.parametrize("ws", [2, 3], ids=["sbarrier", "grpbar"])
+def test_fwd_wave_specialised_equals_per_sample(gpu, H, W, cin, n, dt, ws):
     """The wave-specialised forward against the per-sample kernel on the same inputs: y, the
     statistics and out agree up to the order of the f32 sums (the bias enters the accumulators
     first instead of last: at most one 16-bit rounding step apart), and with more samples than
@@ -96,7 +97,7 @@ def test_fwd_wave_specialised_equals_per_sample(gpu, H, W, cin, n, dt):
     res = torch.randn(n, P, 96, device=gpu).to(dt)
     dmask = (torch.rand(n, 96, device=gpu) > 0.05).float() / 0.95
     outs = []
-    for var in (1, 2):
+    for var in (1, ws):
         with kernel_variant(VARIANT_FWD, var):
             outs.append(conv_gn_fwd(x, w, b, g, be, H, W, res=res, dmask=dmask, want_mask=True))
     (o1, y1, s1, m1), (o2, y2, s2, m2) = outs
@@ -154,9 +155,15 @@ def test_conv_gn_bwd_matches_torch(gpu, H, W, cin, n, with_res, dt):
         ref_out = conv_gn_bwd(dout, out, y, st, g, x, H, W, wT=wT, dmask=dmask, addend=add, want_dz=with_res)
     for a_, b_ in zip(ref_rm, ref_out):
         assert (a_ is None and b_ is None) or torch.equal(a_, b_)
-    # wave-specialised vs per-sample: the same sums in another order (channel sums folded 21 -> 11)
-    for a_, b_ in zip((dx, dz, dw, dgn), ref_rm):
-        assert (a_ is None and b_ is None) or _rel(a_, b_) < 2e-3
+    # the wave-specialised kernels vs per-sample: the same sums in another order (channel sums
+    # folded 21 -> 11)
+    if want_dx and H * W <= 256:
+        for ws in (2, 3):
+            with kernel_variant(VARIANT_BWD, ws):
+                got = conv_gn_bwd(dout, None, y, st, g, x, H, W, wT=wT, dmask=dmask, addend=add, want_dz=with_res,
+                                  rmask=rm)
+            for a_, b_ in zip(got, ref_rm):
+                assert (a_ is None and b_ is None) or _rel(a_, b_) < 2e-3, ws
     nchw = lambda t, c: t.float().view(n, H, W, c).permute(0, 3, 1, 2).contiguous()  # noqa: E731
     nhwc = lambda t: t.permute(0, 2, 3, 1).reshape(n, P, -1)  # noqa: E731
     xr = nchw(x, cin)

@@ -16,6 +16,7 @@ ap.add_argument("--n", type=int, default=32768)
 ap.add_argument("--hw", default="16x16")
 ap.add_argument("--cin", type=int, default=96)
 ap.add_argument("--dtype", default="fp16")
+ap.add_argument("--variant", type=int, default=2, help="2: s_barrier form, 3: grp_bar form")
 args = ap.parse_args()
 import torch  # noqa: E402
 from ms_amd import _lib as L  # noqa: E402
@@ -33,7 +34,7 @@ wt = prep_weight(w, cin, dt)
 diag = torch.zeros(4096 * 8, dtype=torch.int64, device=dev)
 lib = L.load()
 lib.mc_set_fwd_diag.argtypes = [ctypes.c_void_p]
-with kernel_variant(VARIANT_FWD, 2):
+with kernel_variant(VARIANT_FWD, args.variant):
     for _ in range(2):
         conv_gn_fwd(x, wt, b, g, be, H, W, res=res, want_mask=True)
     torch.cuda.synchronize()
@@ -41,7 +42,7 @@ with kernel_variant(VARIANT_FWD, 2):
     conv_gn_fwd(x, wt, b, g, be, H, W, res=res, want_mask=True)
     torch.cuda.synchronize()
     lib.mc_set_fwd_diag(None)
-d = diag.view(-1, 2, 24).cpu().double()
+d = diag[: (diag.numel() // 48) * 48].view(-1, 2, 24).cpu().double()
 d = d[d[:, 0].sum(1) > 0]
 grid = d.shape[0]
 per = d.mean(0) / (n / grid)  # ticks per sample per workgroup

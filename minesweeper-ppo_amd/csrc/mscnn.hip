@@ -510,29 +510,36 @@ __global__ __launch_bounds__(512, 1) void k_conv_gn_fwd_ws(FwdParams<E> p) {
     if (GB) grp_bar(&sCnt[0], gbt += 4u, lane); \
     else WS_BAR(seg);                      \
   } while (0)
-    u32x4 wr[NWC];
-    auto wload = [&](int tap) {
+    // Weight taps are prefetched WPF taps ahead into WPF register sets (set = tap mod WPF, static in
+    // the unrolled tap loop): the conv waves' weight loads share the CU's vector-memory path with
+    // the memory waves' HBM streams and queue behind them, so one tap of cover (~1.2k cycles of
+    // MFMA) is not enough.
+    constexpr int WPF = 3;
+    static_assert(9 % WPF == 0, "tap sets repeat per sample");
+    u32x4 wr[WPF][NWC];
+    auto wload = [&](int tap, u32x4 (&w)[NWC]) {
       const u32x4* ws = reinterpret_cast<const u32x4*>(p.wt + (size_t)tap * COUT * CIN);
 #pragma unroll
       for (int k = 0; k < NWC; ++k) {
         const int i = ctid + 256 * k;
-        if (k < COUT * C8 / 256 || i < COUT * C8) wr[k] = ws[i];
+        if (k < COUT * C8 / 256 || i < COUT * C8) w[k] = ws[i];
       }
     };
-    auto wstore = [&](int slot) {
+    auto wstore = [&](int slot, const u32x4 (&w)[NWC]) {
       E* sw = sRing + slot * COUT * CINP;
 #pragma unroll
       for (int k = 0; k < NWC; ++k) {
         const int i = ctid + 256 * k;
         if (k < COUT * C8 / 256 || i < COUT * C8) {
           const int co = i / C8, c8 = i - co * C8;
-          *reinterpret_cast<u32x4*>(&sw[co * CINP + c8 * 8]) = wr[k];
+          *reinterpret_cast<u32x4*>(&sw[co * CINP + c8 * 8]) = w[k];
         }
       }
     };
-    wload(0);
-    wstore(0);
-    wload(1);
+    wload(0, wr[0]);
+    wstore(0, wr[0]);
+#pragma unroll
+    for (int k = 1; k <= WPF; ++k) wload(k % 9, wr[k % WPF]);
     int qr[NPT], qc[NPT];
     bool qv[NPT];
 #pragma unroll
@@ -564,12 +571,17 @@ __global__ __launch_bounds__(512, 1) void k_conv_gn_fwd_ws(FwdParams<E> p) {
               for (int e = 0; e < 4; ++e) acc[t][ct][4 * j + e] = b4[e];
           }
       }
-      for (int tap = 0; tap < 9; ++tap) {
+#pragma unroll 1
+      for (int t3 = 0; t3 < 9; t3 += WPF)
+#pragma unroll
+      for (int u = 0; u < WPF; ++u) {  // (the register set index (tap + 1) mod WPF is static)
+        const int tap = t3 + u;
         if (tap) CONV_BAR(tap - 1);  // T_tap: the ring slot of this tap is written, the other one free
         if (!conv) continue;
         const int g = it * 9 + tap;
-        if (g + 1 < total) wstore((g + 1) & 1);  // registers hold tap (g+1) mod 9
-        if (g + 2 < total) wload((tap + 2) % 9);
+        // set (tap+1) mod WPF holds tap (g+1) mod 9; refill it with tap g+1+WPF
+        if (g + 1 < total) wstore((g + 1) & 1, wr[(u + 1) % WPF]);
+        if (g + 1 + WPF < total) wload((tap + 1 + WPF) % 9, wr[(u + 1) % WPF]);
         const E* sW = sRing + (g & 1) * COUT * CINP;
         const int dr = tap / 3 - 1, dc = tap % 3 - 1;
         int aoff[NPT];

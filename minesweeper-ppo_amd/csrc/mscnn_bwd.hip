@@ -406,29 +406,33 @@ __global__ __launch_bounds__(512, 1) void k_bwd_data_ws(BwdDataParams<E> p) {
   if (wave < WAVES) {
     // =============================== dgrad waves ===============================
     const int ctid = threadIdx.x, l32 = lane & 31, hh = lane >> 5;
-    u32x4 wr[NWC];
-    auto wload = [&](int tap) {
+    // W^T taps prefetched WPF taps ahead (as the forward's conv waves: their loads queue behind
+    // the memory waves' HBM streams in the CU's vector-memory path)
+    constexpr int WPF = 3;
+    u32x4 wr[WPF][NWC];
+    auto wload = [&](int tap, u32x4 (&w)[NWC]) {
       const u32x4* ws = reinterpret_cast<const u32x4*>(p.wT + (size_t)tap * COUT * COUT);
 #pragma unroll
       for (int k = 0; k < NWC; ++k) {
         const int i = ctid + 256 * k;
-        if (k < COUT * NC8 / 256 || i < COUT * NC8) wr[k] = ws[i];
+        if (k < COUT * NC8 / 256 || i < COUT * NC8) w[k] = ws[i];
       }
     };
-    auto wstore = [&](int slot) {
+    auto wstore = [&](int slot, const u32x4 (&w)[NWC]) {
       E* sw = sRing + slot * COUT * DCP;
 #pragma unroll
       for (int k = 0; k < NWC; ++k) {
         const int i = ctid + 256 * k;
         if (k < COUT * NC8 / 256 || i < COUT * NC8) {
           const int ci = i / NC8, k8 = i - ci * NC8;
-          *reinterpret_cast<u32x4*>(&sw[ci * DCP + k8 * 8]) = wr[k];
+          *reinterpret_cast<u32x4*>(&sw[ci * DCP + k8 * 8]) = w[k];
         }
       }
     };
-    wload(0);
-    wstore(0);
-    wload(1);
+    wload(0, wr[0]);
+    wstore(0, wr[0]);
+#pragma unroll
+    for (int k = 1; k <= WPF; ++k) wload(k % 9, wr[k % WPF]);
     if (ctid < 2) sCnt[ctid] = 0u;
     unsigned gbt = 0u;
     int qr[NPT], qc[NPT];
@@ -452,15 +456,19 @@ __global__ __launch_bounds__(512, 1) void k_bwd_data_ws(BwdDataParams<E> p) {
         for (int ct = 0; ct < 3; ++ct)
 #pragma unroll
           for (int i = 0; i < 16; ++i) acc[t][ct][i] = 0.f;
-      for (int tap = 0; tap < 9; ++tap) {
+#pragma unroll 1
+      for (int t3 = 0; t3 < 9; t3 += WPF)
+#pragma unroll
+      for (int u = 0; u < WPF; ++u) {
+        const int tap = t3 + u;
         if (tap) {  // T_tap
           if (GB) grp_bar(&sCnt[0], gbt += 4u, lane);
           else lds_barrier();
         }
         if (!conv) continue;
         const int g = it * 9 + tap;
-        if (g + 1 < total) wstore((g + 1) & 1);
-        if (g + 2 < total) wload((tap + 2) % 9);
+        if (g + 1 < total) wstore((g + 1) & 1, wr[(u + 1) % WPF]);
+        if (g + 1 + WPF < total) wload((tap + 1 + WPF) % 9, wr[(u + 1) % WPF]);
         const E* sW = sRing + (g & 1) * COUT * DCP;
         const int dr = tap / 3 - 1, dc = tap % 3 - 1;
         int aoff[NPT];

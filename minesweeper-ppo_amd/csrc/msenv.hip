@@ -1709,29 +1709,86 @@ __device__ __forceinline__ Pcg keyed_late_pcg(uint64_t seed, uint64_t gidx, uint
   return L;
 }
 
+// Late-start clicks on wave-uniform packed row words (compile-time boards of <= 4 words: 16x16,
+// 9x9, 8x8): lanes -> words through LDS (sRow: the wave's 64-entry row buffer), and back.
+template <int H_, int W_>
+__device__ __forceinline__ void late_rows_to_words(uint64_t row, uint64_t (&w)[4], uint64_t* sRow, int lane) {
+  constexpr int RPW = 64 / W_, NW = (H_ + RPW - 1) / RPW;
+  sRow[lane] = row;
+  wave_sync();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    uint64_t acc = 0ull;
+    if (i < NW) {
+#pragma unroll
+      for (int k = 0; k < RPW; ++k)
+        if (i * RPW + k < H_) acc |= sRow[i * RPW + k] << (k * W_);
+    }
+    w[i] = rfl64(acc);  // (every lane read the same bytes)
+  }
+  wave_sync();
+}
+template <int H_, int W_>
+__device__ __forceinline__ uint64_t late_words_row(const uint64_t (&w)[4], int lane) {
+  constexpr int RPW = 64 / W_;
+  const int wi = lane / RPW;
+  uint64_t v = w[0];
+  v = wi == 1 ? w[1] : v;
+  v = wi == 2 ? w[2] : v;
+  v = wi == 3 ? w[3] : v;
+  return lane < H_ ? (v >> ((lane - wi * RPW) * W_)) & ((1ull << W_) - 1ull) : 0ull;
+}
+
 // One env's _apply_late_start (env.py:421-466) with the late generator L (wave-uniform),
 // its clicks wave-parallel as in k_step; writes the env's state and its reset obs / mask.
+// An env's state as late_env reads it: its rows in lanes and its meta (wave-uniform). k_late
+// loads the next env's state before running the current one, so the load round trip of a
+// reset overlaps the previous reset's clicks instead of heading the serial chain.
+struct LateState {
+  uint64_t mine, rev;
+  uint64_t st_hi, st_lo, inc_hi, inc_lo;
+  uint32_t has32, uinteger, step_count, flags;
+};
+
+template <int H_, int W_>
+__device__ __forceinline__ LateState late_load(const KParams& p, int64_t env, const Geo<H_, W_>& g, int lane) {
+  const int NW = g.NW();
+  const EnvMeta* mp = p.meta + env;
+  LateState s;
+  s.mine = load_row(p.mine_words + env * NW, g, lane);
+  s.rev = load_row(p.rev_words + env * NW, g, lane);
+  s.st_hi = rfl64(mp->st_hi);
+  s.st_lo = rfl64(mp->st_lo);
+  s.inc_hi = rfl64(mp->inc_hi);
+  s.inc_lo = rfl64(mp->inc_lo);
+  s.has32 = rfl(mp->has32);
+  s.uinteger = rfl(mp->uinteger);
+  s.step_count = rfl((uint32_t)mp->step_count);
+  s.flags = rfl(mp->flags);
+  return s;
+}
+
 template <int H_, int W_>
 __device__ __forceinline__ void late_env(const KParams& p, Pcg& L, const LateCfg& lc, int64_t env,
-                                         const uint64_t (&J)[4], uint64_t* sR, uint64_t* sM, uint32_t* sTab,
-                                         const Geo<H_, W_>& g, int lane) {
+                                         const LateState& st, const uint64_t (&J)[4], uint64_t* sR, uint64_t* sM,
+                                         uint32_t* sTab, const Geo<H_, W_>& g, int lane) {
   const int H = g.H, A = g.A(), NW = g.NW();
   const uint64_t rowmask = g.rowmask();
   const int safe_total = A - p.K;
   EnvMeta* mp = p.meta + env;
   uint64_t* mwords = p.mine_words + env * NW;
   uint64_t* rwords = p.rev_words + env * NW;
-  uint64_t mine = load_row(mwords, g, lane);
-  uint64_t rev = load_row(rwords, g, lane);
+  uint64_t mine = st.mine;
+  uint64_t rev = st.rev;
   Pcg rng;
-  rng.hi = rfl64(mp->st_hi);
-  rng.lo = rfl64(mp->st_lo);
-  rng.ihi = rfl64(mp->inc_hi);
-  rng.ilo = rfl64(mp->inc_lo);
-  rng.has32 = rfl(mp->has32);
-  rng.uinteger = rfl(mp->uinteger);
-  int32_t step_count = (int32_t)rfl((uint32_t)mp->step_count);
-  bool fc = (rfl(mp->flags) & 1u) != 0;
+  rng.hi = st.st_hi;
+  rng.lo = st.st_lo;
+  rng.ihi = st.inc_hi;
+  rng.ilo = st.inc_lo;
+  rng.has32 = st.has32;
+  rng.uinteger = st.uinteger;
+  int32_t step_count = (int32_t)st.step_count;
+  bool fc = (st.flags & 1u) != 0;
   // prob <= 0 short-circuits before the draw (env.py:421)
   if (lc.prob > 0.0 && (double)(pcg_next64(L) >> 11) * 0x1.0p-53 < lc.prob) {
     bool success = false;
@@ -1760,6 +1817,80 @@ __device__ __forceinline__ void late_env(const KParams& p, Pcg& L, const LateCfg
       // episode only by a win. The mines are fixed now: their zero-cell map is built once.
       const uint64_t Um = wave_shr1(mine) | wave_shl1(mine);
       const uint64_t zero = ~(Um | (Um << 1) | (Um >> 1) | (mine << 1) | (mine >> 1)) & rowmask;
+      constexpr bool SCALAR = H_ > 0 && W_ > 0 && W_ <= 32 && (H_ + 64 / (W_ ? W_ : 1) - 1) / (64 / (W_ ? W_ : 1)) <= 4;
+      if constexpr (SCALAR) {
+        // The same clicks on wave-uniform words (SGPRs): a click is the bounded draw, a k-th set
+        // bit over the candidate words and one bit set -- no cross-lane step; a zero cell's
+        // flood fill runs on the rows and is folded back. Bit order in the words is row-major.
+        constexpr int RPW = 64 / W_, NWS = (H_ + RPW - 1) / RPW;
+        uint64_t rw[4], mw[4], zw[4], cw[4], vw[4];
+        late_rows_to_words<H_, W_>(rev, rw, sR, lane);
+        late_rows_to_words<H_, W_>(mine, mw, sR, lane);
+        late_rows_to_words<H_, W_>(zero, zw, sR, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          uint64_t v = 0ull;
+#pragma unroll
+          for (int k = 0; k < RPW; ++k)
+            if (i * RPW + k < H_) v |= ((1ull << W_) - 1ull) << (k * W_);
+          vw[i] = v;
+          cw[i] = ~mw[i] & ~rw[i] & vw[i];
+        }
+        for (int k = 0; k < lc.max_extra_steps; ++k) {
+          if (safe_total - revealed <= target) {
+            success = true;
+            break;
+          }
+          uint32_t kk = pcg_bounded(L, (uint32_t)(safe_total - revealed) - 1u);  // rng.choice (row-major)
+          uint64_t x = cw[0];
+          int wi = 0;
+#pragma unroll
+          for (int i = 0; i + 1 < NWS; ++i) {
+            const uint32_t pc = (uint32_t)__popcll(x);
+            if (wi == i && kk >= pc) {
+              kk -= pc;
+              x = cw[i + 1];
+              wi = i + 1;
+            }
+          }
+          const int bit = select_bit64(x, kk);
+          const uint64_t b = 1ull << bit;
+          uint64_t zsel = zw[0];
+#pragma unroll
+          for (int i = 1; i < NWS; ++i) zsel = wi == i ? zw[i] : zsel;
+          if ((zsel & b) == 0ull) {  // a cell with adjacent mines: reveals itself alone
+#pragma unroll
+            for (int i = 0; i < NWS; ++i)
+              if (wi == i) {
+                rw[i] |= b;
+                cw[i] &= ~b;
+              }
+            revealed += 1;
+          } else {  // flood_fill_reveal from a zero cell on the rows, folded back into the words
+            rev = late_words_row<H_, W_>(rw, lane);
+            const int cr = wi * RPW + bit / W_, cc = bit - (bit / W_) * W_;
+            const uint64_t allow = ~mine & ~rev & (lane < H ? rowmask : 0ull);
+            uint64_t Fr = (lane == cr) ? (1ull << cc) : 0ull;
+            while (true) {
+              const uint64_t S = Fr & zero;
+              const uint64_t Dh = S | (S << 1) | (S >> 1);
+              const uint64_t Dv = Dh | wave_shr1(Dh) | wave_shl1(Dh);
+              const uint64_t Fn = Fr | (Dv & allow);
+              const bool changed = __ballot(Fn != Fr) != 0ull;
+              Fr = Fn;
+              if (!changed) break;
+            }
+            revealed += (int)wave_sum((uint32_t)__popcll(Fr));
+            late_rows_to_words<H_, W_>(rev | Fr, rw, sR, lane);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) cw[i] = ~mw[i] & ~rw[i] & vw[i];
+          }
+          step_count += 1;
+          done = revealed >= safe_total;  // a win (env.py:133-140)
+          if (done) break;
+        }
+        rev = late_words_row<H_, W_>(rw, lane);
+      } else
       for (int k = 0; k < lc.max_extra_steps; ++k) {
         if (safe_total - revealed <= target) {
           success = true;
@@ -1850,15 +1981,31 @@ __global__ __launch_bounds__(64) void k_late(KParams p, Pcg* lstate, LateCfg lc,
   L.uinteger = lstate->uinteger;
   uint64_t J[4];
   load_jump(p.jump, lane, J);
-  // the flags of 64 envs per load and ballot (one dependent scalar load per env cost ~0.5 us each)
-  for (int64_t base = 0; base < p.n; base += kWave) {
-    const int64_t e = base + lane;
-    uint64_t todo = __ballot(e < p.n && (!need || need[e]));
-    while (todo) {
-      const int l = __ffsll((unsigned long long)todo) - 1;
-      todo &= todo - 1ull;
-      late_env(p, L, lc, base + l, J, sR, sM, sTab, g, lane);
+  // the flags of 64 envs per load and ballot (one dependent scalar load per env cost ~0.5 us each);
+  // the next env's state is loaded before the current env runs
+  int64_t base = -kWave;
+  uint64_t todo = 0ull;
+  auto next_env = [&]() -> int64_t {
+    while (todo == 0ull) {
+      base += kWave;
+      if (base >= p.n) return -1;
+      const int64_t e = base + lane;
+      todo = __ballot(e < p.n && (!need || need[e]));
     }
+    const int l = __ffsll((unsigned long long)todo) - 1;
+    todo &= todo - 1ull;
+    return base + l;
+  };
+  int64_t cur = next_env();
+  LateState sc = {};
+  if (cur >= 0) sc = late_load(p, cur, g, lane);
+  while (cur >= 0) {
+    const int64_t nxt = next_env();
+    LateState sn = sc;
+    if (nxt >= 0) sn = late_load(p, nxt, g, lane);
+    late_env(p, L, lc, cur, sc, J, sR, sM, sTab, g, lane);
+    cur = nxt;
+    sc = sn;
   }
   if (lane == 0) {
     lstate->hi = L.hi;
@@ -1884,7 +2031,7 @@ __global__ __launch_bounds__(64) void k_late_keyed(KParams p, LateCfg lc, uint64
   load_jump(p.jump, lane, J);
   const EnvMeta* mp = p.meta + env;
   Pcg L = keyed_late_pcg(seed, (uint64_t)(env_begin + env), rfl64(mp->st_hi), rfl64(mp->st_lo));
-  late_env(p, L, lc, env, J, sR, sM, sTab, g, lane);
+  late_env(p, L, lc, env, late_load(p, env, g, lane), J, sR, sM, sTab, g, lane);
 }
 
 // ---------------------------------------------------------------------------

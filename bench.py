@@ -329,6 +329,9 @@ def ppo_bench(args, world, rank, local_rank, dev):
             "updates_per_s": 1.0 / spu, "s_per_update": spu,
             "samples_per_s": n_loc * world * T / spu, "envs_total": n_loc * world, "steps_per_env": T,
             "rollout_s": mean("rollout_s"), "gae_s": mean("gae_s"), "ppo_s": mean("ppo_s"),
+            # the reference's rollout timing buckets (train_rl.py:278-288), GPU time per update
+            "rollout_buckets_s": {k[len("rollout_"):]: mean(k) for k in sorted(prof[-1]) if k.startswith("rollout_")
+                                  and k.endswith("_total_s")},
             "amp": args.amp, "rollout_buffer_obs": "u8 cell codes" if tr.obs_codes else "f32 one-hot",
             "model": "cnn_residual 96ch x 5 blocks (950,947 params)",
             "roofline": {"bound": "mfma", "achieved": gflop / spu / 1e3, "peak": BF16_DENSE_PEAK_TFLOPS,

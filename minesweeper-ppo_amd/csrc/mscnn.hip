@@ -453,6 +453,15 @@ __host__ __device__ inline size_t ws_lds_bytes(int P) {
     dwait[(seg)] += t1_ - t0_;                               \
     tprev = t1_;                                             \
   } while (0)
+#define WS_GBAR(seg, cnt, tgt)                               \
+  do {                                                       \
+    const unsigned long long t0_ = __builtin_amdgcn_s_memtime(); \
+    grp_bar((cnt), (tgt), lane);                             \
+    const unsigned long long t1_ = __builtin_amdgcn_s_memtime(); \
+    dwork[(seg)] += t0_ - tprev;                             \
+    dwait[(seg)] += t1_ - t0_;                               \
+    tprev = t1_;                                             \
+  } while (0)
 #define WS_DIAG_OUT(role)                                                                   \
   do {                                                                                      \
     if (p.diag && (threadIdx.x & 255) == 0)                                                 \
@@ -464,6 +473,7 @@ __host__ __device__ inline size_t ws_lds_bytes(int P) {
 #else
 #define WS_DIAG_DECL do { } while (0)
 #define WS_BAR(seg) lds_barrier()
+#define WS_GBAR(seg, cnt, tgt) grp_bar((cnt), (tgt), lane)
 #define WS_DIAG_OUT(role) do { } while (0)
 #endif
 
@@ -507,7 +517,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_gn_fwd_ws(FwdParams<E> p) {
     unsigned gbt = 0u;  // GB: this role's barriers passed x 4
 #define CONV_BAR(seg)                      \
   do {                                     \
-    if (GB) grp_bar(&sCnt[0], gbt += 4u, lane); \
+    if (GB) WS_GBAR(seg, &sCnt[0], gbt += 4u); \
     else WS_BAR(seg);                      \
   } while (0)
     // Weight taps are prefetched WPF taps ahead into WPF register sets (set = tap mod WPF, static in
@@ -823,7 +833,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_gn_fwd_ws(FwdParams<E> p) {
           epi(np, rg, 1);
           epi(np, rg, 2);
         }
-        grp_bar(&sCnt[1], gbt += 4u, lane);  // every memory wave's reads of y(it-1) done
+        WS_GBAR(0, &sCnt[1], gbt += 4u);  // every memory wave's reads of y(it-1) done
         if (it + 1 < cnt) xstore(rg);
         if (it + 2 < cnt) xload((int)blockIdx.x + (it + 2) * G);
         if (it < cnt && p.res) rload((int)blockIdx.x + it * G);

@@ -1709,38 +1709,6 @@ __device__ __forceinline__ Pcg keyed_late_pcg(uint64_t seed, uint64_t gidx, uint
   return L;
 }
 
-// Late-start clicks on wave-uniform packed row words (compile-time boards of <= 4 words: 16x16,
-// 9x9, 8x8): lanes -> words through LDS (sRow: the wave's 64-entry row buffer), and back.
-template <int H_, int W_>
-__device__ __forceinline__ void late_rows_to_words(uint64_t row, uint64_t (&w)[4], uint64_t* sRow, int lane) {
-  constexpr int RPW = 64 / W_, NW = (H_ + RPW - 1) / RPW;
-  sRow[lane] = row;
-  wave_sync();
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    uint64_t acc = 0ull;
-    if (i < NW) {
-#pragma unroll
-      for (int k = 0; k < RPW; ++k)
-        if (i * RPW + k < H_) acc |= sRow[i * RPW + k] << (k * W_);
-    }
-    w[i] = rfl64(acc);  // (every lane read the same bytes)
-  }
-  wave_sync();
-}
-template <int H_, int W_>
-__device__ __forceinline__ uint64_t late_words_row(const uint64_t (&w)[4], int lane) {
-  constexpr int RPW = 64 / W_;
-  const int wi = lane / RPW;
-  uint64_t v = w[0];
-  v = wi == 1 ? w[1] : v;
-  v = wi == 2 ? w[2] : v;
-  v = wi == 3 ? w[3] : v;
-  return lane < H_ ? (v >> ((lane - wi * RPW) * W_)) & ((1ull << W_) - 1ull) : 0ull;
-}
-
-// One env's _apply_late_start (env.py:421-466) with the late generator L (wave-uniform),
-// its clicks wave-parallel as in k_step; writes the env's state and its reset obs / mask.
 // An env's state as late_env reads it: its rows in lanes and its meta (wave-uniform). k_late
 // loads the next env's state before running the current one, so the load round trip of a
 // reset overlaps the previous reset's clicks instead of heading the serial chain.
@@ -1817,80 +1785,6 @@ __device__ __forceinline__ void late_env(const KParams& p, Pcg& L, const LateCfg
       // episode only by a win. The mines are fixed now: their zero-cell map is built once.
       const uint64_t Um = wave_shr1(mine) | wave_shl1(mine);
       const uint64_t zero = ~(Um | (Um << 1) | (Um >> 1) | (mine << 1) | (mine >> 1)) & rowmask;
-      constexpr bool SCALAR = H_ > 0 && W_ > 0 && W_ <= 32 && (H_ + 64 / (W_ ? W_ : 1) - 1) / (64 / (W_ ? W_ : 1)) <= 4;
-      if constexpr (SCALAR) {
-        // The same clicks on wave-uniform words (SGPRs): a click is the bounded draw, a k-th set
-        // bit over the candidate words and one bit set -- no cross-lane step; a zero cell's
-        // flood fill runs on the rows and is folded back. Bit order in the words is row-major.
-        constexpr int RPW = 64 / W_, NWS = (H_ + RPW - 1) / RPW;
-        uint64_t rw[4], mw[4], zw[4], cw[4], vw[4];
-        late_rows_to_words<H_, W_>(rev, rw, sR, lane);
-        late_rows_to_words<H_, W_>(mine, mw, sR, lane);
-        late_rows_to_words<H_, W_>(zero, zw, sR, lane);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          uint64_t v = 0ull;
-#pragma unroll
-          for (int k = 0; k < RPW; ++k)
-            if (i * RPW + k < H_) v |= ((1ull << W_) - 1ull) << (k * W_);
-          vw[i] = v;
-          cw[i] = ~mw[i] & ~rw[i] & vw[i];
-        }
-        for (int k = 0; k < lc.max_extra_steps; ++k) {
-          if (safe_total - revealed <= target) {
-            success = true;
-            break;
-          }
-          uint32_t kk = pcg_bounded(L, (uint32_t)(safe_total - revealed) - 1u);  // rng.choice (row-major)
-          uint64_t x = cw[0];
-          int wi = 0;
-#pragma unroll
-          for (int i = 0; i + 1 < NWS; ++i) {
-            const uint32_t pc = (uint32_t)__popcll(x);
-            if (wi == i && kk >= pc) {
-              kk -= pc;
-              x = cw[i + 1];
-              wi = i + 1;
-            }
-          }
-          const int bit = select_bit64(x, kk);
-          const uint64_t b = 1ull << bit;
-          uint64_t zsel = zw[0];
-#pragma unroll
-          for (int i = 1; i < NWS; ++i) zsel = wi == i ? zw[i] : zsel;
-          if ((zsel & b) == 0ull) {  // a cell with adjacent mines: reveals itself alone
-#pragma unroll
-            for (int i = 0; i < NWS; ++i)
-              if (wi == i) {
-                rw[i] |= b;
-                cw[i] &= ~b;
-              }
-            revealed += 1;
-          } else {  // flood_fill_reveal from a zero cell on the rows, folded back into the words
-            rev = late_words_row<H_, W_>(rw, lane);
-            const int cr = wi * RPW + bit / W_, cc = bit - (bit / W_) * W_;
-            const uint64_t allow = ~mine & ~rev & (lane < H ? rowmask : 0ull);
-            uint64_t Fr = (lane == cr) ? (1ull << cc) : 0ull;
-            while (true) {
-              const uint64_t S = Fr & zero;
-              const uint64_t Dh = S | (S << 1) | (S >> 1);
-              const uint64_t Dv = Dh | wave_shr1(Dh) | wave_shl1(Dh);
-              const uint64_t Fn = Fr | (Dv & allow);
-              const bool changed = __ballot(Fn != Fr) != 0ull;
-              Fr = Fn;
-              if (!changed) break;
-            }
-            revealed += (int)wave_sum((uint32_t)__popcll(Fr));
-            late_rows_to_words<H_, W_>(rev | Fr, rw, sR, lane);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) cw[i] = ~mw[i] & ~rw[i] & vw[i];
-          }
-          step_count += 1;
-          done = revealed >= safe_total;  // a win (env.py:133-140)
-          if (done) break;
-        }
-        rev = late_words_row<H_, W_>(rw, lane);
-      } else
       for (int k = 0; k < lc.max_extra_steps; ++k) {
         if (safe_total - revealed <= target) {
           success = true;

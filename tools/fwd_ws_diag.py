@@ -47,6 +47,9 @@ d = d[d[:, 0].sum(1) > 0]
 grid = d.shape[0]
 per = d.mean(0) / (n / grid)  # ticks per sample per workgroup
 segs = [f"tap {k}" for k in range(9)] + ["stats p2", "coef/next"]
+if args.variant == 3:  # grp_bar form: the memory waves' segment 0 = epilogue, segment 10 = staging + loads
+    segs[0] = "tap 0 | mem: epilogue"
+    segs[10] = "coef | mem: x, loads"
 print(f"grid {grid} workgroups, {n / grid:.1f} samples each; s_memtime ticks per sample:")
 print(f"{'segment':10s} {'conv work':>10s} {'conv wait':>10s} {'mem work':>10s} {'mem wait':>10s}")
 tot = torch.zeros(4, dtype=torch.float64)

@@ -25,8 +25,11 @@ int ms_set_debug_flags(ms_handle* h, uint32_t flags);
 /* Kernel variants of the fused CNN layer (mscnn.h), for same-process A/B runs and for the
  * parity tests of every path: kernel 0 = mc_conv_gn_fwd, 1 = mc_conv_gn_bwd; variant 0 =
  * the dispatcher's choice (default), 1 = the per-sample kernel (two 256-thread workgroups
- * per CU), 2 = the wave-specialised kernel (one 512-thread workgroup per CU: conv waves +
- * memory waves) where the board fits it (P <= 256). Process-wide, not thread-safe. */
+ * per CU), 2 / 3 = the pixel-split wave-specialised kernel (one 512-thread workgroup per CU:
+ * conv waves + memory waves; s_barrier / LDS-counter group barriers), 4 / 5 = the forward's
+ * channel-split wave-specialised kernel (3 conv waves of 32 output channels each, LDS-DMA weight
+ * rings, 4 memory waves; B operands single- / double-buffered), where the board fits them
+ * (P <= 256). Process-wide, not thread-safe. */
 #define MC_VAR_FWD 0
 #define MC_VAR_BWD 1
 int mc_set_variant(int32_t kernel, int32_t variant);

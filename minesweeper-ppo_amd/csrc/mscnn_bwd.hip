@@ -410,12 +410,15 @@ __global__ __launch_bounds__(512, 1) void k_bwd_data_ws(BwdDataParams<E> p) {
     // the memory waves' HBM streams in the CU's vector-memory path)
     constexpr int WPF = 3;
     u32x4 wr[WPF][NWC];
+    // every load unconditional (a clamped chunk index for the partial last chunk): the waitcnt
+    // pass then sees the same number of loads per tap and waits only for the set it stores,
+    // instead of vmcnt(0) behind a conditionally skipped load
     auto wload = [&](int tap, u32x4 (&w)[NWC]) {
       const u32x4* ws = reinterpret_cast<const u32x4*>(p.wT + (size_t)tap * COUT * COUT);
 #pragma unroll
       for (int k = 0; k < NWC; ++k) {
         const int i = ctid + 256 * k;
-        if (k < COUT * NC8 / 256 || i < COUT * NC8) w[k] = ws[i];
+        w[k] = ws[i < COUT * NC8 ? i : COUT * NC8 - 1];
       }
     };
     auto wstore = [&](int slot, const u32x4 (&w)[NWC]) {
@@ -468,7 +471,7 @@ __global__ __launch_bounds__(512, 1) void k_bwd_data_ws(BwdDataParams<E> p) {
         if (!conv) continue;
         const int g = it * 9 + tap;
         if (g + 1 < total) wstore((g + 1) & 1, wr[(u + 1) % WPF]);
-        if (g + 1 + WPF < total) wload((tap + 1 + WPF) % 9, wr[(u + 1) % WPF]);
+        wload((tap + 1 + WPF) % 9, wr[(u + 1) % WPF]);  // (past the last tap: unused, harmless)
         const E* sW = sRing + (g & 1) * COUT * DCP;
         const int dr = tap / 3 - 1, dc = tap % 3 - 1;
         int aoff[NPT];

@@ -45,7 +45,8 @@ PROD = [pytest.param(16, 16, 96, 32768, id="c2-16x16-32768"), pytest.param(16, 1
                                        (16, 30, 96, 9), (5, 7, 16, 3)] + PROD)
 @pytest.mark.parametrize("with_res", [False, True])
 @pytest.mark.parametrize("dt", DT)
-@pytest.mark.parametrize("variant", [0, 2, 3], ids=["dispatch", "ws-sbarrier", "ws-grpbar"])
+@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5], ids=["dispatch", "ws-sbarrier", "ws-grpbar", "ws-chsplit",
+                                                      "ws-chsplit-db"])
 def test_conv_gn_fwd_matches_torch(gpu, H, W, cin, n, with_res, dt, variant):
     """The fused forward (conv + bias + GroupNorm + affine [+ residual] + ReLU [+ dropout
     scale]) and its ReLU bitmask vs a torch fp32 reference of the same op, on the dispatcher's
@@ -82,7 +83,7 @@ def _fwd_case(gpu, H, W, cin, n, with_res, dt):
 @pytest.mark.parametrize("H,W,cin,n", [(16, 16, 96, 2000), (16, 16, 16, 700), (9, 9, 96, 900), (12, 12, 96, 300),
                                        (5, 7, 16, 5)])
 @pytest.mark.parametrize("dt", DT)
-@pytest.mark.parametrize("ws", [2, 3], ids=["sbarrier", "grpbar"])
+@pytest.mark.parametrize("ws", [2, 3, 4, 5], ids=["sbarrier", "grpbar", "chsplit", "chsplit-db"])
 def test_fwd_wave_specialised_equals_per_sample(gpu, H, W, cin, n, dt, ws):
     """The wave-specialised forward against the per-sample kernel on the same inputs: y, the
     statistics and out agree up to the order of the f32 sums (the bias enters the accumulators

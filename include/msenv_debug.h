@@ -19,6 +19,7 @@ extern "C" {
 #define MS_DBG_ONE_BOARD_PER_WAVE 4u     /* ms_step: k_step (one board per wave) even where the
                                             lane-packed k_step_packed applies (9x9, 8x8, K<=16) */
 #define MS_DBG_TWO_BOARDS_PER_WAVE 8u    /* k_step_packed with two boards per wave (32-lane groups) */
+#define MS_DBG_FORCE_PACKED 16u          /* 16x16: k_step_packed at any env count (default: >= 16384) */
 
 int ms_set_debug_flags(ms_handle* h, uint32_t flags);
 

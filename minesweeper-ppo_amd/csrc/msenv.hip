@@ -31,6 +31,7 @@
 #include <string.h>
 
 #include <new>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/msenv.h"
@@ -1160,6 +1161,169 @@ __device__ void place_serial_packed(Pcg& rng, uint32_t& mine_out, const Block& B
   mine_out = set_row(s0, s1, r, g);
 }
 
+// Placement of one packed 16x16 board for K <= 48 (same draws and result as place_fixpoint):
+// lane r of the board owns Floyd iterations r, r + 16, r + 32 and computes PCG64 outputs
+// r + 1, r + 17, r + 33 from its one jump entry (k = r + 1) in three chunks of 16 (a chunk's
+// base state is lane 15's state of the previous one). The outputs' words go to the board's LDS
+// scratch, so iteration i reads its draw by index; "t_i repeats an earlier t" is an atomicMin
+// into the board's 256-entry table, the collision chain follows k = t_i - (pop - K) by
+// ds_bpermute (place_fixpoint's closed form), and the mine rows are LDS ORs. Returns false on a
+// Lemire rejection, leaving rng untouched (the caller then runs place_serial_packed_w).
+// scr: the wave's scratch, [4 boards][A] table | [4][96] output words | [4][16] rows.
+template <int H_, int W_>
+__device__ bool place_packed3(Pcg& rng, uint32_t& mine_out, const Block& B, int K, const uint64_t (&J)[4],
+                              uint32_t* scr, int lane) {
+  constexpr int A = H_ * W_;
+  static_assert(H_ <= 16 && A <= 256, "16 rows, 8-bit cells");
+  const int r = lane & 15, bb = lane >> 4;
+  uint32_t* tab = scr + bb * A;
+  uint32_t* xw = scr + 4 * A + bb * 96;
+  uint32_t* rows = scr + 4 * A + 4 * 96 + bb * 16;
+  const int pop = B.pop;
+  const int z0 = (pop == K) ? 1 : 0;
+  const int nF = K - z0;
+  const int D = nF + (K - 1);
+  const int h0 = rng.has32 ? 1 : 0;
+  const int rem = D - h0;
+  const int n_out = (rem + 1) >> 1;  // <= K <= 48
+  const uint64_t ci_lo = J[3] * rng.ilo;
+  const uint64_t ci_hi = __umul64hi(J[3], rng.ilo) + J[3] * rng.ihi + J[2] * rng.ilo;
+  Out o[3];
+  o[0] = jump_out(rng.hi, rng.lo, J[0], J[1], ci_hi, ci_lo);
+#pragma unroll
+  for (int c = 1; c < 3; ++c)
+    o[c] = jump_out(board_read64<16>(o[c - 1].sh, lane, 15), board_read64<16>(o[c - 1].sl, lane, 15), J[0], J[1],
+                    ci_hi, ci_lo);
+  // Lemire rejection test of every consumed draw (exact test only where a leftover is low)
+  uint32_t lft[7], bnd[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    lft[k] = 0xffffffffu;
+    bnd[k] = 0u;
+  }
+  if (h0 && D > 0) {
+    bnd[6] = (nF > 0) ? (uint32_t)(pop - K + z0) : (uint32_t)(K - 1);
+    lft[6] = (uint32_t)((uint64_t)rng.uinteger * (bnd[6] + 1u));
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const int q = 16 * c + r + 1;
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int pidx = h0 + 2 * (q - 1) + hf;
+      if (q <= n_out && pidx < D) {
+        const uint32_t d = hf ? (uint32_t)(o[c].x >> 32) : (uint32_t)o[c].x;
+        bnd[2 * c + hf] = pidx < nF ? (uint32_t)(pop - K + z0 + pidx) : (uint32_t)(K - 1 - (pidx - nF));
+        lft[2 * c + hf] = (uint32_t)((uint64_t)d * (bnd[2 * c + hf] + 1u));
+      }
+    }
+  }
+  bool maybe = false;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) maybe |= lemire_maybe(lft[k], bnd[k]);
+  if (__ballot(maybe) != 0ull) {
+    bool rej = false;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) rej |= lemire_rejects(lft[k], bnd[k]);
+    if (board_any<16>(rej, lane)) return false;
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    xw[32 * c + 2 * r] = (uint32_t)o[c].x;
+    xw[32 * c + 2 * r + 1] = (uint32_t)(o[c].x >> 32);
+  }
+#pragma unroll
+  for (int k = 0; k < A / 16; ++k) tab[16 * k + r] = 0xffffffffu;
+  wave_sync();
+  int t[3], jj[3];
+  bool valid[3];
+#pragma unroll
+  for (int s2 = 0; s2 < 3; ++s2) {
+    const int i = r + 16 * s2;
+    valid[s2] = i < K;
+    jj[s2] = pop - K + i;
+    const int pidx = i - z0;
+    const int idx = pidx - h0;  // word of the fresh outputs (output idx / 2, half idx & 1)
+    uint32_t d = xw[idx < 0 ? 0 : (idx > 95 ? 95 : idx)];
+    if (h0 && pidx == 0) d = rng.uinteger;
+    t[s2] = (valid[s2] && i >= z0) ? (int)(((uint64_t)d * (uint32_t)(jj[s2] + 1)) >> 32) : 0;
+    if (valid[s2]) atomicMin(&tab[t[s2]], (uint32_t)i);
+  }
+  wave_sync();
+  bool dup[3], col[3], kv[3];
+  int ks[3];
+#pragma unroll
+  for (int s2 = 0; s2 < 3; ++s2) {
+    const int i = r + 16 * s2;
+    dup[s2] = valid[s2] && tab[t[s2]] != (uint32_t)i;
+    ks[s2] = t[s2] - (pop - K);  // t_i == j_ks
+    kv[s2] = valid[s2] && ks[s2] >= 0 && ks[s2] < i;
+    col[s2] = dup[s2];
+  }
+  while (true) {
+    bool changed = false, nc[3];
+#pragma unroll
+    for (int s2 = 0; s2 < 3; ++s2) {
+      // every lane of the board takes part: ds_bpermute returns 0 from an EXEC-disabled source
+      const int src = ks[s2] & 15, sl = (ks[s2] >> 4) & 3;
+      const uint32_t c0 = board_read<16>(col[0] ? 1u : 0u, lane, src);
+      const uint32_t c1 = board_read<16>(col[1] ? 1u : 0u, lane, src);
+      const uint32_t c2 = board_read<16>(col[2] ? 1u : 0u, lane, src);
+      const uint32_t cs = sl == 0 ? c0 : (sl == 1 ? c1 : c2);
+      nc[s2] = dup[s2] || (kv[s2] && cs != 0u);
+      changed |= nc[s2] != col[s2];
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 3; ++s2) col[s2] = nc[s2];
+    if (__ballot(changed) == 0ull) break;
+  }
+  rows[r] = 0u;
+  wave_sync();
+#pragma unroll
+  for (int s2 = 0; s2 < 3; ++s2)
+    if (valid[s2]) {
+      const int cell = map_block<W_>(col[s2] ? jj[s2] : t[s2], B);
+      atomicOr(&rows[cell / W_], 1u << (cell % W_));
+    }
+  wave_sync();
+  mine_out = r < H_ ? rows[r] : 0u;
+  wave_sync();
+  if (n_out > 0) {  // the state after the last consumed output (board-uniform chunk c, lane lr)
+    const int lq = n_out - 1, c = lq >> 4, lr = lq & 15;
+    const uint64_t sh = c == 0 ? o[0].sh : (c == 1 ? o[1].sh : o[2].sh);
+    const uint64_t sl = c == 0 ? o[0].sl : (c == 1 ? o[1].sl : o[2].sl);
+    const uint64_t x = c == 0 ? o[0].x : (c == 1 ? o[1].x : o[2].x);
+    rng.hi = board_read64<16>(sh, lane, lr);
+    rng.lo = board_read64<16>(sl, lane, lr);
+    rng.uinteger = board_read<16>((uint32_t)(x >> 32), lane, lr);
+  }
+  if (D > 0) rng.has32 = (uint32_t)(rem & 1);
+  return true;
+}
+
+// Serial reference-order placement of one packed board of up to 256 cells (the Lemire
+// fallback of place_packed3): every lane of the board runs the same draws.
+template <int H_, int W_>
+__device__ void place_serial_packed_w(Pcg& rng, uint32_t& mine_out, const Block& B, int K, int r) {
+  static_assert(64 % W_ == 0 && H_ * W_ <= 256, "rows inside one 64-bit word");
+  uint64_t s0 = 0ull, s1 = 0ull, s2 = 0ull, s3 = 0ull;
+  auto word = [&](uint32_t c) -> uint64_t& { return c < 64u ? s0 : (c < 128u ? s1 : (c < 192u ? s2 : s3)); };
+  for (int j = B.pop - K; j < B.pop; ++j) {
+    uint32_t c = (uint32_t)map_block<W_>((int)pcg_bounded(rng, (uint32_t)j), B);
+    if ((word(c) >> (c & 63u)) & 1ull) c = (uint32_t)map_block<W_>(j, B);
+    word(c) |= 1ull << (c & 63u);
+  }
+  for (int i = K - 1; i >= 1; --i) (void)pcg_bounded(rng, (uint32_t)i);  // shuffle draws
+  const uint32_t c0 = (uint32_t)(r * W_);
+  mine_out = r < H_ ? (uint32_t)((word(c0) >> (c0 & 63u)) & ((1ull << W_) - 1ull)) : 0u;
+}
+
+// 16x16 boards four to a wave (k_step_packed): 16 rows in a 16-lane DPP row, K <= 48
+template <int H_, int W_>
+constexpr bool packable16() {
+  return H_ == 16 && W_ == 16;
+}
+
 template <int H_, int W_>
 constexpr bool packable() {
   // W_ <= 30: pk_emit's neighbour count shifts a u32 row by up to W_ + 1 bits
@@ -1191,6 +1355,16 @@ struct PackedLds {
   uint32_t rev[kWave];                  // revealed rows for the word store
 };
 
+// LDS of one wave of the 16x16 packed kernel: no byte image (pk_emit16 stores straight from
+// the rows), the placement scratch of place_packed3, rows for the word store
+template <int H_, int W_, int BPW>
+struct PackedLds16 {
+  static constexpr int A = H_ * W_;
+  uint32_t scr[4 * (A + 96 + 16)];
+  alignas(16) uint32_t row[kWave];
+  uint32_t rev[kWave];
+};
+
 // One reveal on each board of the wave (env.py:103-137 minus the reward / step bookkeeping):
 // first-click placement, mine hit, flood fill, win check. Per-board results are uniform
 // across the board's lanes.
@@ -1212,8 +1386,13 @@ __device__ __forceinline__ void pk_click(const KParams& p, Pcg& rng, uint32_t& m
     if (!fc) {
       const Block B = make_block<H_, W_>(cell, ar, ac, p.K, p.guarantee != 0);
       bool ok = false;
-      if (!(p.dbg_flags & MS_DBG_FORCE_SERIAL_PLACEMENT)) ok = place_packed<H_, W_, LPB>(rng, mine, B, p.K, J, sRow, lane, dgs);
-      if (!ok) place_serial_packed(rng, mine, B, p.K, g, r);
+      if constexpr (packable16<H_, W_>()) {
+        if (!(p.dbg_flags & MS_DBG_FORCE_SERIAL_PLACEMENT)) ok = place_packed3<H_, W_>(rng, mine, B, p.K, J, sRow, lane);
+        if (!ok) place_serial_packed_w<H_, W_>(rng, mine, B, p.K, r);
+      } else {
+        if (!(p.dbg_flags & MS_DBG_FORCE_SERIAL_PLACEMENT)) ok = place_packed<H_, W_, LPB>(rng, mine, B, p.K, J, sRow, lane, dgs);
+        if (!ok) place_serial_packed(rng, mine, B, p.K, g, r);
+      }
       fc = true;
       mines_changed = true;
     }
@@ -1325,11 +1504,55 @@ __device__ __forceinline__ void pk_emit(float* ob, uint8_t* mb, int nbl, uint32_
   }
 }
 
+// Observation + action mask of the wave's nbl live 16x16 boards without an LDS image: per
+// board, lane l covers row l / 4, cells 4 (l % 4) .. +3, fetching that row and its two
+// neighbours from the board's lanes; each of the 10 channel planes is then one 1 KiB float4
+// store of the wave and the mask one 256-B dword store. Same bytes as pk_emit (env.py:172-196).
+template <int H_, int W_, int BPW>
+__device__ __forceinline__ void pk_emit16(float* ob, uint8_t* mb, int nbl, uint32_t mine, uint32_t rev, bool fc,
+                                          int lane) {
+  static_assert(H_ == 16 && W_ == 16, "16x16 boards");
+  constexpr int A = H_ * W_;
+  const int row = lane >> 2, c0 = 4 * (lane & 3);
+#pragma unroll
+  for (int b = 0; b < BPW; ++b) {
+    if (b >= nbl) break;  // (wave-uniform)
+    const int src = 16 * b + row;
+    const uint32_t m = bperm(mine, src), rv = bperm(rev, src);
+    const uint32_t mu0 = bperm(mine, (src - 1) & 63), md0 = bperm(mine, (src + 1) & 63);
+    const uint32_t mu = row > 0 ? mu0 : 0u, md = row < 15 ? md0 : 0u;
+    const bool f = bperm(fc ? 1u : 0u, 16 * b) != 0u;
+    const uint32_t m1 = m << 1, up1 = mu << 1, dn1 = md << 1;
+    uint32_t cnt[4], rb[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = c0 + e;
+      cnt[e] = (uint32_t)__popc((up1 >> c) & 7u) + (uint32_t)__popc((dn1 >> c) & 7u) + ((m1 >> c) & 1u) +
+               ((m1 >> (c + 2)) & 1u);
+      rb[e] = (rv >> c) & 1u;
+    }
+    if (ob) {
+      float4* o4 = reinterpret_cast<float4*>(ob + (size_t)b * 10 * A) + lane;
+#pragma unroll
+      for (int ch = 0; ch < 10; ++ch) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          v[e] = ch == 0 ? (float)rb[e] : ((f && rb[e] && cnt[e] + 1u == (uint32_t)ch) ? 1.f : 0.f);
+        o4[ch * (A / 4)] = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+    if (mb)
+      reinterpret_cast<uint32_t*>(mb + (size_t)b * A)[lane] =
+          (rb[0] ^ 1u) | ((rb[1] ^ 1u) << 8) | ((rb[2] ^ 1u) << 16) | ((rb[3] ^ 1u) << 24);
+  }
+}
+
 // EnvMeta and the row words of each live board (rows -> packed words through LDS)
-template <int H_, int W_, int BPW, int LPB>
+template <int H_, int W_, int BPW, int LPB, class Lds>
 __device__ __forceinline__ void pk_store_state(EnvMeta* mp, uint64_t* mwords, uint64_t* rwords, const Pcg& rng,
                                                int32_t step_count, bool fc, uint32_t mine, uint32_t rev,
-                                               bool mines_changed, bool live, PackedLds<H_, W_, BPW>& S, int lane) {
+                                               bool mines_changed, bool live, Lds& S, int lane) {
   constexpr int RPW = 64 / W_;
   constexpr int NW = (H_ + RPW - 1) / RPW;
   const int r = lane & (LPB - 1);
@@ -1387,16 +1610,18 @@ __device__ __forceinline__ void pk_load(const KParams& p, int64_t env, int r, ui
 template <int H_, int W_, int WPG, int BPW>
 __global__ __launch_bounds__(64 * WPG) void k_step_packed(KParams p) {
   constexpr int LPB = kWave / BPW;  // lanes per board (the board's rows: its first H)
+  constexpr bool BIG = packable16<H_, W_>();  // 16x16: place_packed3 + pk_emit16
   static_assert(BPW == 2 || BPW == 4, "boards per wave");
-  static_assert(packable<H_, W_>(), "packed board shape");
+  static_assert(packable<H_, W_>() || (BIG && BPW == 4), "packed board shape");
   constexpr int A = H_ * W_;
   constexpr int RPW = 64 / W_;
   constexpr int NW = (H_ + RPW - 1) / RPW;
-  __shared__ PackedLds<H_, W_, BPW> S_all[WPG];
+  using Lds = std::conditional_t<BIG, PackedLds16<H_, W_, BPW>, PackedLds<H_, W_, BPW>>;
+  __shared__ Lds S_all[WPG];
   const int lane = lane_id();
   const int r = lane & (LPB - 1);
   const int wv = (WPG == 1) ? 0 : (int)rfl(threadIdx.x >> 6);
-  PackedLds<H_, W_, BPW>& S = S_all[wv];
+  Lds& S = S_all[wv];
   const int64_t env0 = ((int64_t)blockIdx.x * WPG + wv) * BPW;
   const bool wave_live = env0 < p.n;
   const int64_t env_raw = env0 + (lane / LPB);
@@ -1422,7 +1647,10 @@ __global__ __launch_bounds__(64 * WPG) void k_step_packed(KParams p) {
   bool done, mines_changed = false, cell_rev;
   int outcome;
   uint32_t newly, total_rev;
-  pk_click<H_, W_, LPB>(p, rng, mine, rev, fc, (int)cell64, J, S.row, lane, dgs, done, outcome, newly, total_rev,
+  uint32_t* scr;
+  if constexpr (BIG) scr = S.scr;
+  else scr = S.row;
+  pk_click<H_, W_, LPB>(p, rng, mine, rev, fc, (int)cell64, J, scr, lane, dgs, done, outcome, newly, total_rev,
                         mines_changed, cell_rev);
   DSTAMP(3);
   double reward = 0.0;
@@ -1440,9 +1668,16 @@ __global__ __launch_bounds__(64 * WPG) void k_step_packed(KParams p) {
   }
   DSTAMP(4);
   const int nbl = (p.n - env0 < BPW) ? (int)(p.n - env0) : BPW;  // live boards of this wave
-  if (p.obs || p.mask)
-    pk_emit<H_, W_, BPW, LPB>(p.obs ? p.obs + env0 * 10 * A : nullptr, p.mask ? p.mask + env0 * A : nullptr, nbl,
-                              mine, rev, fc, S, lane, dgs);
+  if constexpr (BIG) {
+    if (p.obs || p.mask)
+      pk_emit16<H_, W_, BPW>(p.obs ? p.obs + env0 * 10 * A : nullptr, p.mask ? p.mask + env0 * A : nullptr, nbl, mine,
+                             rev, fc, lane);
+    DSTAMP(9);
+  } else {
+    if (p.obs || p.mask)
+      pk_emit<H_, W_, BPW, LPB>(p.obs ? p.obs + env0 * 10 * A : nullptr, p.mask ? p.mask + env0 * A : nullptr, nbl,
+                                mine, rev, fc, S, lane, dgs);
+  }
   pk_store_state<H_, W_, BPW, LPB>(p.meta + env, p.mine_words + env * NW, p.rev_words + env * NW, rng, step_count, fc,
                                    mine, rev, mines_changed, live, S, lane);
   DSTAMP(5);
@@ -2391,8 +2626,25 @@ bool shape_ok(const ms_cfg* c) {
 
 // ev0/ev1 non-null (ms_set_timing_events): the dispatch itself stamps the events, so their
 // difference is the kernel's execution time as the profiler sees it (no launch gap)
+// 16x16 boards four to a wave from this many envs on: measured 2-4 % faster than the one-board
+// kernel at 65,536, within +-3 % at 8,192-32,768 and 10 % slower at 4,096 (both store-bound at
+// 32k+, the one-board kernel's 4x more waves hide latency better at 4k; profiles/r04/
+// packed16_step.txt); MS_DBG_FORCE_PACKED takes the packed kernel at any count
+constexpr int64_t kPack16MinEnvs = 65536;
+
 template <int H_, int W_>
 void launch_step(const KParams& p, int epw, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+  if constexpr (packable16<H_, W_>()) {
+    if (p.K >= 1 && p.K <= 48 &&
+        !(p.dbg_flags & (MS_DBG_ONE_BOARD_PER_WAVE | MS_DBG_FORCE_CHAIN_PLACEMENT | MS_DBG_TWO_BOARDS_PER_WAVE)) &&
+        (p.n >= kPack16MinEnvs || (p.dbg_flags & MS_DBG_FORCE_PACKED)) && ((uintptr_t)p.obs & 15u) == 0 &&
+        ((uintptr_t)p.mask & 3u) == 0 && !p.codes) {
+      constexpr int WPG = 4;
+      const unsigned grid = (unsigned)((p.n + 4 * WPG - 1) / (4 * WPG));
+      hipExtLaunchKernelGGL((k_step_packed<H_, W_, WPG, 4>), dim3(grid), dim3(64 * WPG), 0, s, ev0, ev1, 0, p);
+      return;
+    }
+  }
   if constexpr (packable<H_, W_>()) {
     // small boards: four per wave (k_step_packed); its float4 / dword stores need a
     // 16-B obs and 4-B mask base

@@ -71,6 +71,7 @@ MS_DBG_FORCE_SERIAL_PLACEMENT = 1
 MS_DBG_FORCE_CHAIN_PLACEMENT = 2
 MS_DBG_ONE_BOARD_PER_WAVE = 4  # ms_step without the lane-packed small-board kernel
 MS_DBG_TWO_BOARDS_PER_WAVE = 8  # the lane-packed kernel with 32-lane groups
+MS_DBG_FORCE_PACKED = 16  # 16x16: the lane-packed kernel below its env-count threshold too
 _RESTYPES = {"ms_last_error": ctypes.c_char_p, "ms_abi_version": ctypes.c_int32}
 
 

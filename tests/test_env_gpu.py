@@ -305,6 +305,55 @@ def test_packed_step_equals_one_board_per_wave(gpu, H, W, K, N, mode):
         assert torch.equal(sa[k], sb[k]), k
 
 
+@pytest.mark.parametrize("K,N", [(40, 203), (40, 4), (40, 1), (48, 66), (1, 37), (10, 64), (47, 130)])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_packed16_step_equals_one_board_per_wave(gpu, K, N, mode):
+    """16x16 boards four to a wave (k_step_packed with place_packed3 and pk_emit16; forced below
+    its env-count threshold) are bit-exact with k_step: every output, the boards and the RNG
+    state, including the serial placement fallback; K = 48 / 47 fill the three Floyd slots per
+    lane, K = 1 the first; N = 203 / 130 / 37 leave a partial last wave."""
+    from ms_amd import _lib as L
+    a, b, c = (_vec(16, 16, K, N, seed=23) for _ in range(3))
+    a.set_debug_flags(L.MS_DBG_FORCE_PACKED)
+    b.set_debug_flags(L.MS_DBG_ONE_BOARD_PER_WAVE)
+    c.set_debug_flags(L.MS_DBG_FORCE_PACKED | L.MS_DBG_FORCE_SERIAL_PLACEMENT)
+    for v in (a, b, c):
+        v.reset()
+    for t in range(60):
+        act = a.tape_actions(t, mode)
+        outs = [v.step(act) for v in (a, b, c)]
+        for o in outs[1:]:
+            assert torch.equal(outs[0][0]["obs"], o[0]["obs"]), t
+            assert torch.equal(outs[0][0]["action_mask"], o[0]["action_mask"]), t
+            assert torch.equal(outs[0][1], o[1]) and torch.equal(outs[0][2], o[2]), t
+            for k, x in outs[0][3].tensors.items():
+                assert torch.equal(x, o[3].tensors[k]), (t, k)
+        st = a.rng_state()
+        assert all(np.array_equal(st, v.rng_state()) for v in (b, c)), t
+    sa, sb = a.snapshot_tensors(), b.snapshot_tensors()
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
+
+
+def test_packed16_default_dispatch_at_65536(gpu):
+    """At 65,536 16x16x40 envs the dispatcher takes the packed kernel by itself (no flag); it
+    stays bit-exact with the one-board kernel over 25 steps (N = 65,538 leaves a partial wave)."""
+    from ms_amd import _lib as L
+    N = 65538
+    a, b = _vec(16, 16, 40, N, seed=5), _vec(16, 16, 40, N, seed=5)
+    b.set_debug_flags(L.MS_DBG_ONE_BOARD_PER_WAVE)
+    a.reset()
+    b.reset()
+    for t in range(25):
+        act = a.tape_actions(t, 0)
+        (ba, ra, da, ia), (bb, rb, db, ib) = a.step(act), b.step(act)
+        assert torch.equal(ba["obs"], bb["obs"]) and torch.equal(ba["action_mask"], bb["action_mask"]), t
+        assert torch.equal(ra, rb) and torch.equal(da, db), t
+        for k, x in ia.tensors.items():
+            assert torch.equal(x, ib.tensors[k]), (t, k)
+    assert np.array_equal(a.rng_state(), b.rng_state())
+
+
 def test_packed_step_misaligned_obs_falls_back(gpu):
     """An obs base that is not 16-B aligned (a view one float in) takes k_step; results equal."""
     from ms_amd import _lib as L

@@ -141,7 +141,17 @@ struct HeadBwdParams {
   float* part;        // [gridDim][PART]
   int64_t M;
   int P;
+  int exp;            // MC_WSX builds: timing experiments (HBX_* bits; results wrong)
 };
+// timing experiments of k_heads_bwd (libmsenv_wsx.so, mc_set_heads_exp; tools/heads_bwd_exp.py):
+// each bit removes one part so its cost can be read off the launch time
+#ifdef MC_WSX
+#define HBX(bit) ((p.exp & (bit)) != 0)
+#else
+#define HBX(bit) false
+#endif
+[[maybe_unused]] constexpr int HBX_NO_DF_STORE = 1, HBX_NO_DW1 = 2, HBX_NO_H = 4, HBX_NO_FLOAD = 8,
+                               HBX_NO_DH_WRITE = 16, HBX_NO_DF = 32;
 
 // f tile [128][96]: 16-B chunk ch of row r at chunk ch ^ ((r >> 2) & 3)
 __device__ __forceinline__ int sf_off(int r, int col) {
@@ -195,7 +205,7 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
       for (int i = 0; i < NFC; ++i) {
         const int c = tid + 256 * i + zo, r = c / 12, ch = c - r * 12;
         const int64_t row = base + r < p.M ? base + r : p.M - 1;
-        v[i] = *reinterpret_cast<const u32x4*>(&p.f[row * C + ch * 8]);
+        v[i] = HBX(HBX_NO_FLOAD) ? u32x4{(uint32_t)c, 0u, 0u, 0u} : *reinterpret_cast<const u32x4*>(&p.f[row * C + ch * 8]);
       }
       const int64_t rowd = base + (tid & (TRB - 1)) < p.M ? base + (tid & (TRB - 1)) : p.M - 1;
       const float d0 = p.dlp[rowd];
@@ -222,7 +232,7 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
         for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
       const int ra = pt * 32 + l32 + zo;
 #pragma unroll 1
-      for (int ks = 0; ks < 6; ++ks) {
+      for (int ks = 0; ks < (HBX(HBX_NO_H) ? 0 : 6); ++ks) {
         const E8 a = *reinterpret_cast<const E8*>(&L.f[sf_off(ra, ks * 16 + 8 * hh)]);
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
@@ -243,7 +253,7 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
           dw2acc[j] += hv * dl;
           const float dh = hv > 0.f ? dl * w2c : 0.f;
           db1acc[j] += dh;
-          L.dh[sd_off(pr, c)] = (E)dh;
+          if (!HBX(HBX_NO_DH_WRITE)) L.dh[sd_off(pr, c)] = (E)dh;
         }
       }
     }
@@ -272,7 +282,7 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
           for (int i = 0; i < 16; ++i) acc2[u][i] = 0.f;
       }
 #pragma unroll 1
-      for (int ks = 0; ks < 6; ++ks) {
+      for (int ks = 0; ks < (HBX(HBX_NO_DF) ? 0 : 6); ++ks) {
         const E8 b = *reinterpret_cast<const E8*>(&L.dh[sd_off(rb, ks * 16 + 8 * hh)]);
         const int r0 = ks * 16 + 8 * (g >> 1) + q + zo;  // W1 rows (K = c), transposed read
 #pragma unroll
@@ -284,7 +294,7 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
       }
       // acc2[u][r] = df[px = rb][k = (KT0+u)*32 + 8*(r>>2) + 4*hh + (r&3)]: 8-B stores (staging
       // them in LDS for 16-B stores needs the f region, i.e. dW1 first: 3.26 ms, spills)
-      if (row < p.M) {
+      if (row < p.M && !HBX(HBX_NO_DF_STORE)) {
         typedef typename EV<E>::v4 E4;
 #pragma unroll
         for (int u = 0; u < NKT; ++u)
@@ -299,7 +309,7 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
 
     // ---- dW1[c][k] += sum_px dh[px][c] f[px][k] over the tile's 64 rows ----
 #pragma unroll 1
-    for (int kk = 0; kk < TRB / 16; ++kk) {
+    for (int kk = 0; kk < (HBX(HBX_NO_DW1) ? 0 : TRB / 16); ++kk) {
       const int r0 = kk * 16 + 8 * (g >> 1) + q + zo;
       E8 av[6], bv[3];
 #pragma unroll
@@ -420,6 +430,10 @@ int run_heads_fwd(const uint16_t* f, const uint16_t* w1, const float* b1, const 
   return check("k_heads_fwd");
 }
 
+#ifdef MC_WSX
+int g_heads_exp = 0;
+#endif
+
 template <typename E>
 int run_heads_bwd(const uint16_t* f, const float* dlp, const float* dlm, const uint16_t* w1, const uint16_t* w1pT,
                   const float* b1, const float* w2, const float* gadd, int32_t P, uint16_t* df, float* dw1, float* db1,
@@ -437,6 +451,10 @@ int run_heads_bwd(const uint16_t* f, const float* dlp, const float* dlm, const u
   p.part = work;
   p.M = M;
   p.P = P;
+  p.exp = 0;
+#ifdef MC_WSX
+  p.exp = g_heads_exp;
+#endif
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)k_heads_bwd<E>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -454,6 +472,11 @@ int run_heads_bwd(const uint16_t* f, const float* dlp, const float* dlm, const u
 }  // namespace
 
 extern "C" {
+
+#ifdef MC_WSX
+// timing experiments only (tools/heads_bwd_exp.py): HBX_* bits of the next k_heads_bwd launches
+void mc_set_heads_exp(int32_t e) { g_heads_exp = e; }
+#endif
 
 int mc_heads_fwd(const uint16_t* f, const uint16_t* w1, const float* b1, const float* w2, const float* b2,
                  float* out_p, float* out_m, int64_t M, int32_t dtype, void* stream) {

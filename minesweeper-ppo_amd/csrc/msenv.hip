@@ -1779,11 +1779,17 @@ __global__ __launch_bounds__(256) void k_rng_state(const EnvMeta* meta, int64_t 
 // ---------------------------------------------------------------------------
 // ms_tape_actions: synthetic policy, one wave per env.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int select_bit(uint64_t x, uint32_t k) {  // k-th set bit (0-based)
-  for (uint32_t i = 0; i < k; ++i) x &= x - 1ull;
-  return __ffsll((unsigned long long)x) - 1;
-}
 
+
+// exclusive prefix sum inside each 16-lane row (row_shr 1/2/4/8)
+__device__ __forceinline__ uint32_t row_excl_scan16(uint32_t v) {
+  uint32_t s = v;
+  s += dpp32<0x111>(s);
+  s += dpp32<0x112>(s);
+  s += dpp32<0x114>(s);
+  s += dpp32<0x118>(s);
+  return s - v;
+}
 
 // exclusive prefix sum over the wave: Kogge-Stone inside 16-lane rows
 // (row_shr 1/2/4/8), then row_bcast15 / row_bcast31 carry across rows (GFX9 DPP)
@@ -1809,6 +1815,20 @@ __device__ __forceinline__ int select_bit64(uint64_t x, uint32_t k) {  // k-th s
   for (int half = 32; half >= 1; half >>= 1) {
     const uint64_t lowmask = (1ull << half) - 1ull;
     const uint32_t c = (uint32_t)__popcll(x & lowmask);
+    if (k >= c) {
+      k -= c;
+      x >>= half;
+      pos += half;
+    }
+  }
+  return pos;
+}
+
+__device__ __forceinline__ int select_bit32(uint32_t x, uint32_t k) {  // k-th set bit, k < popc(x)
+  int pos = 0;
+#pragma unroll
+  for (int half = 16; half >= 1; half >>= 1) {
+    const uint32_t c = (uint32_t)__popc(x & ((1u << half) - 1u));
     if (k >= c) {
       k -= c;
       x >>= half;
@@ -1971,10 +1991,38 @@ __device__ __forceinline__ LateState late_load(const KParams& p, int64_t env, co
   return s;
 }
 
+// MS_DIAG builds: k_late's cycle accounting (tools/late_diag.py), summed over the launch in dacc:
+// [0] whole launch, [1] envs visited, [2] late starts, [3] envs without a late start (draw + stores
+// + emit), [4] first clicks (placement included), [5] extra-click loops, [6] extra clicks,
+// [7] of them flood fills, [8] flood iterations, [9] late envs' stores + emit, [10] attempts
+#ifdef MS_DIAG
+#define LSTAMP(k)                                          \
+  do {                                                     \
+    if (dacc) {                                            \
+      const uint64_t t_ = __builtin_amdgcn_s_memtime();    \
+      dacc[(k)] += t_ - tl_;                               \
+      tl_ = t_;                                            \
+    }                                                      \
+  } while (0)
+#define LCOUNT(k, v)            \
+  do {                          \
+    if (dacc) dacc[(k)] += (v); \
+  } while (0)
+#else
+#define LSTAMP(k) do { } while (0)
+#define LCOUNT(k, v) do { } while (0)
+#endif
+
 template <int H_, int W_>
 __device__ __forceinline__ void late_env(const KParams& p, Pcg& L, const LateCfg& lc, int64_t env,
                                          const LateState& st, const uint64_t (&J)[4], uint64_t* sR, uint64_t* sM,
-                                         uint32_t* sTab, const Geo<H_, W_>& g, int lane) {
+                                         uint32_t* sTab, const Geo<H_, W_>& g, int lane, uint64_t* dacc = nullptr) {
+  (void)dacc;
+#ifdef MS_DIAG
+  uint64_t tl_ = __builtin_amdgcn_s_memtime();
+  LCOUNT(1, 1);
+#endif
+  bool late = false;
   const int H = g.H, A = g.A(), NW = g.NW();
   const uint64_t rowmask = g.rowmask();
   const int safe_total = A - p.K;
@@ -1994,8 +2042,11 @@ __device__ __forceinline__ void late_env(const KParams& p, Pcg& L, const LateCfg
   bool fc = (st.flags & 1u) != 0;
   // prob <= 0 short-circuits before the draw (env.py:421)
   if (lc.prob > 0.0 && (double)(pcg_next64(L) >> 11) * 0x1.0p-53 < lc.prob) {
+    late = true;
+    LCOUNT(2, 1);
     bool success = false;
     for (int att = 0; att < lc.max_attempts && !success; ++att) {
+      LCOUNT(10, 1);
       if (fc) {  // env.reset() (env.py:87-101): the env's own RNG continues
         mine = 0ull;
         rev = 0ull;
@@ -2008,6 +2059,7 @@ __device__ __forceinline__ void late_env(const KParams& p, Pcg& L, const LateCfg
       uint32_t nw, tr;
       board_click(rng, mine, rev, fc, first, p, J, sTab, sR, g, lane, done, oc, nw, tr, mc);
       step_count += 1;
+      LSTAMP(4);
       if (done) continue;
       int target = lc.min_hidden + (int)pcg_bounded(L, (uint32_t)(lc.max_hidden - lc.min_hidden));
       target = target < safe_total ? target : safe_total;
@@ -2029,18 +2081,25 @@ __device__ __forceinline__ void late_env(const KParams& p, Pcg& L, const LateCfg
         const uint64_t cand = ~mine & ~rev & (lane < H ? rowmask : 0ull);
         const uint32_t pc = (uint32_t)__popcll(cand);
         const uint32_t kk = pcg_bounded(L, cnt - 1u);  // rng.choice(flatnonzero(...)) (row-major)
-        const uint32_t before = wave_excl_scan(pc);
+        LCOUNT(6, 1);
+        // boards of <= 16 rows keep their candidates in lanes 0-15: one DPP row scans them
+        const uint32_t before = (H_ && H_ <= 16) ? row_excl_scan16(pc) : wave_excl_scan(pc);
         const bool mine_lane = kk >= before && kk < before + pc;
         const uint64_t who = __ballot(mine_lane);
         const int src = __ffsll((unsigned long long)who) - 1;
-        const int col = (int)readlane32((uint32_t)(mine_lane ? select_bit(cand, kk - before) : 0), src);
+        // the k-th candidate of the row by a popcount bisection (a clear-lowest-bit loop cost ~2x
+        // the whole click: tools/late_diag.py)
+        const int sel = (W_ && W_ <= 32) ? select_bit32((uint32_t)cand, kk - before) : select_bit64(cand, kk - before);
+        const int col = (int)readlane32((uint32_t)(mine_lane ? sel : 0), src);
         if (((readlane64(zero, src) >> col) & 1ull) == 0ull) {
           if (lane == src) rev |= 1ull << col;
           revealed += 1;
         } else {  // flood_fill_reveal (env_numba.py:17-77) from a zero cell, as board_click
           const uint64_t allow = ~mine & ~rev & (lane < H ? rowmask : 0ull);
           uint64_t Fr = (lane == src) ? (1ull << col) : 0ull;
+          LCOUNT(7, 1);
           while (true) {
+            LCOUNT(8, 1);
             const uint64_t S = Fr & zero;
             const uint64_t Dh = S | (S << 1) | (S >> 1);
             const uint64_t Dv = Dh | wave_shr1(Dh) | wave_shl1(Dh);
@@ -2057,6 +2116,7 @@ __device__ __forceinline__ void late_env(const KParams& p, Pcg& L, const LateCfg
         if (done) break;
       }
       if (!success && !done && safe_total - revealed <= target) success = true;
+      LSTAMP(5);
     }
     if (!success) {  // fallback: leave the board fresh (env.py:465-466)
       mine = 0ull;
@@ -2082,6 +2142,8 @@ __device__ __forceinline__ void late_env(const KParams& p, Pcg& L, const LateCfg
              p.codes ? p.codes + env * A : nullptr, sR, sM, fc, g, lane, reinterpret_cast<uint8_t*>(sTab));
   }
   __syncthreads();
+  if (late) LSTAMP(9);
+  else LSTAMP(3);
 }
 
 __device__ __forceinline__ void load_jump(const uint64_t* jump, int lane, uint64_t (&J)[4]) {
@@ -2125,6 +2187,12 @@ __global__ __launch_bounds__(64) void k_late(KParams p, Pcg* lstate, LateCfg lc,
     todo &= todo - 1ull;
     return base + l;
   };
+  uint64_t* dacc = nullptr;
+#ifdef MS_DIAG
+  uint64_t dv[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  if (p.diag) dacc = dv;
+  const uint64_t t_begin = __builtin_amdgcn_s_memtime();
+#endif
   int64_t cur = next_env();
   LateState sc = {};
   if (cur >= 0) sc = late_load(p, cur, g, lane);
@@ -2132,10 +2200,17 @@ __global__ __launch_bounds__(64) void k_late(KParams p, Pcg* lstate, LateCfg lc,
     const int64_t nxt = next_env();
     LateState sn = sc;
     if (nxt >= 0) sn = late_load(p, nxt, g, lane);
-    late_env(p, L, lc, cur, sc, J, sR, sM, sTab, g, lane);
+    late_env(p, L, lc, cur, sc, J, sR, sM, sTab, g, lane, dacc);
     cur = nxt;
     sc = sn;
   }
+#ifdef MS_DIAG
+  if (dacc) {
+    dv[0] = __builtin_amdgcn_s_memtime() - t_begin;
+    if (lane == 0)
+      for (int k = 0; k < 16; ++k) p.diag[k] = dv[k];
+  }
+#endif
   if (lane == 0) {
     lstate->hi = L.hi;
     lstate->lo = L.lo;

@@ -1991,6 +1991,79 @@ __device__ __forceinline__ LateState late_load(const KParams& p, int64_t env, co
   return s;
 }
 
+// The late-start generator of the shared mode as a jump-ahead batch: lane i holds output i + 1 of
+// the batch (and the state after it), computed from the batch's base state with the handle's
+// jump table, so a draw is a readlane instead of a serial 128-bit PCG step (~45 scalar
+// instructions) on the critical chain. The buffered half-word (has32 / uinteger) follows
+// numpy's next_uint32 as in pcg_next32. lr_state() is the PCG64 state after the last consumed
+// output. The keyed mode keeps a plain Pcg (one reset per wave: nothing to batch).
+struct LateRng {
+  Pcg base;           // state before the batch; inc, has32 / uinteger are the generator's own
+  uint32_t xlo, xhi;  // lane i: output i + 1 of the batch
+  uint64_t sh, sl;    // lane i: the state after it
+  int used;           // outputs of the batch consumed (uniform)
+};
+__device__ __forceinline__ void lr_fill(LateRng& R, const uint64_t (&J)[4]) {
+  const uint64_t ci_lo = J[3] * R.base.ilo;
+  const uint64_t ci_hi = __umul64hi(J[3], R.base.ilo) + J[3] * R.base.ihi + J[2] * R.base.ilo;
+  const Out o = jump_out(R.base.hi, R.base.lo, J[0], J[1], ci_hi, ci_lo);
+  R.sh = o.sh;
+  R.sl = o.sl;
+  R.xlo = (uint32_t)o.x;
+  R.xhi = (uint32_t)(o.x >> 32);
+  R.used = 0;
+}
+__device__ __forceinline__ uint64_t lr_next64(LateRng& R, const uint64_t (&J)[4]) {
+  if (R.used == kWave) {
+    R.base.hi = readlane64(R.sh, kWave - 1);
+    R.base.lo = readlane64(R.sl, kWave - 1);
+    lr_fill(R, J);
+  }
+  const int u = R.used++;
+  return ((uint64_t)readlane32(R.xhi, u) << 32) | readlane32(R.xlo, u);
+}
+__device__ __forceinline__ uint64_t lr_next64(Pcg& L, const uint64_t (&J)[4]) {
+  (void)J;
+  return pcg_next64(L);
+}
+__device__ __forceinline__ uint32_t lr_next32(LateRng& R, const uint64_t (&J)[4]) {
+  if (R.base.has32) {
+    R.base.has32 = 0;
+    return R.base.uinteger;
+  }
+  const uint64_t x = lr_next64(R, J);
+  R.base.has32 = 1;
+  R.base.uinteger = (uint32_t)(x >> 32);
+  return (uint32_t)x;
+}
+// random_bounded_uint64(0, j), numpy's buffered Lemire (as pcg_bounded)
+__device__ __forceinline__ uint32_t lr_bounded(LateRng& R, const uint64_t (&J)[4], uint32_t j) {
+  if (j == 0) return 0;
+  const uint32_t excl = j + 1u;
+  uint64_t m = (uint64_t)lr_next32(R, J) * excl;
+  uint32_t left = (uint32_t)m;
+  if (left < excl) {
+    const uint32_t thr = (0xffffffffu - j) % excl;
+    while (left < thr) {
+      m = (uint64_t)lr_next32(R, J) * excl;
+      left = (uint32_t)m;
+    }
+  }
+  return (uint32_t)(m >> 32);
+}
+__device__ __forceinline__ uint32_t lr_bounded(Pcg& L, const uint64_t (&J)[4], uint32_t j) {
+  (void)J;
+  return pcg_bounded(L, j);
+}
+__device__ __forceinline__ Pcg lr_state(const LateRng& R) {
+  Pcg P = R.base;
+  if (R.used > 0) {
+    P.hi = readlane64(R.sh, R.used - 1);
+    P.lo = readlane64(R.sl, R.used - 1);
+  }
+  return P;
+}
+
 // MS_DIAG builds: k_late's cycle accounting (tools/late_diag.py), summed over the launch in dacc:
 // [0] whole launch, [1] envs visited, [2] late starts, [3] envs without a late start (draw + stores
 // + emit), [4] first clicks (placement included), [5] extra-click loops, [6] extra clicks,
@@ -2013,8 +2086,8 @@ __device__ __forceinline__ LateState late_load(const KParams& p, int64_t env, co
 #define LCOUNT(k, v) do { } while (0)
 #endif
 
-template <int H_, int W_>
-__device__ __forceinline__ void late_env(const KParams& p, Pcg& L, const LateCfg& lc, int64_t env,
+template <int H_, int W_, class Rng>
+__device__ __forceinline__ void late_env(const KParams& p, Rng& L, const LateCfg& lc, int64_t env,
                                          const LateState& st, const uint64_t (&J)[4], uint64_t* sR, uint64_t* sM,
                                          uint32_t* sTab, const Geo<H_, W_>& g, int lane, uint64_t* dacc = nullptr) {
   (void)dacc;
@@ -2041,7 +2114,7 @@ __device__ __forceinline__ void late_env(const KParams& p, Pcg& L, const LateCfg
   int32_t step_count = (int32_t)st.step_count;
   bool fc = (st.flags & 1u) != 0;
   // prob <= 0 short-circuits before the draw (env.py:421)
-  if (lc.prob > 0.0 && (double)(pcg_next64(L) >> 11) * 0x1.0p-53 < lc.prob) {
+  if (lc.prob > 0.0 && (double)(lr_next64(L, J) >> 11) * 0x1.0p-53 < lc.prob) {
     late = true;
     LCOUNT(2, 1);
     bool success = false;
@@ -2053,7 +2126,7 @@ __device__ __forceinline__ void late_env(const KParams& p, Pcg& L, const LateCfg
         fc = false;
         step_count = 0;
       }
-      const int first = (int)pcg_bounded(L, (uint32_t)(A - 1));
+      const int first = (int)lr_bounded(L, J, (uint32_t)(A - 1));
       bool done, mc = false;
       int oc;
       uint32_t nw, tr;
@@ -2061,7 +2134,7 @@ __device__ __forceinline__ void late_env(const KParams& p, Pcg& L, const LateCfg
       step_count += 1;
       LSTAMP(4);
       if (done) continue;
-      int target = lc.min_hidden + (int)pcg_bounded(L, (uint32_t)(lc.max_hidden - lc.min_hidden));
+      int target = lc.min_hidden + (int)lr_bounded(L, J, (uint32_t)(lc.max_hidden - lc.min_hidden));
       target = target < safe_total ? target : safe_total;
       target = target > 1 ? target : 1;
       int revealed = (int)tr;
@@ -2072,28 +2145,60 @@ __device__ __forceinline__ void late_env(const KParams& p, Pcg& L, const LateCfg
       // episode only by a win. The mines are fixed now: their zero-cell map is built once.
       const uint64_t Um = wave_shr1(mine) | wave_shl1(mine);
       const uint64_t zero = ~(Um | (Um << 1) | (Um >> 1) | (mine << 1) | (mine >> 1)) & rowmask;
+      // Compile-time boards of <= 256 cells (<= 32 columns, <= 16 rows) keep the candidates
+      // (np.flatnonzero order) as a list in lane registers, four cell indices per lane (byte j of
+      // lane l = entry 4l + j): the k-th is one readlane, and a numbered cell leaves the list by a
+      // one-entry shift; the list is rebuilt from the rows after a flood fill.
+      constexpr bool kList = H_ && W_ && H_ <= 16 && W_ <= 32 && H_ * W_ <= 256;
+      uint32_t lword = 0u;
+      auto build_list = [&]() {
+        uint8_t* lst = reinterpret_cast<uint8_t*>(sTab);
+        uint32_t b = (uint32_t)(~mine & ~rev & (lane < H ? rowmask : 0ull));
+        uint32_t i = row_excl_scan16((uint32_t)__popc(b));
+        while (b) {
+          lst[i++] = (uint8_t)(lane * W_ + __ffs(b) - 1);
+          b &= b - 1u;
+        }
+        wave_sync();
+        lword = reinterpret_cast<const uint32_t*>(lst)[lane];
+        wave_sync();
+      };
+      if constexpr (kList) build_list();
       for (int k = 0; k < lc.max_extra_steps; ++k) {
         if (safe_total - revealed <= target) {
           success = true;
           break;
         }
         const uint32_t cnt = (uint32_t)(safe_total - revealed);
-        const uint64_t cand = ~mine & ~rev & (lane < H ? rowmask : 0ull);
-        const uint32_t pc = (uint32_t)__popcll(cand);
-        const uint32_t kk = pcg_bounded(L, cnt - 1u);  // rng.choice(flatnonzero(...)) (row-major)
+        const uint32_t kk = lr_bounded(L, J, cnt - 1u);  // rng.choice(flatnonzero(...)) (row-major)
         LCOUNT(6, 1);
-        // boards of <= 16 rows keep their candidates in lanes 0-15: one DPP row scans them
-        const uint32_t before = (H_ && H_ <= 16) ? row_excl_scan16(pc) : wave_excl_scan(pc);
-        const bool mine_lane = kk >= before && kk < before + pc;
-        const uint64_t who = __ballot(mine_lane);
-        const int src = __ffsll((unsigned long long)who) - 1;
-        // the k-th candidate of the row by a popcount bisection (a clear-lowest-bit loop cost ~2x
-        // the whole click: tools/late_diag.py)
-        const int sel = (W_ && W_ <= 32) ? select_bit32((uint32_t)cand, kk - before) : select_bit64(cand, kk - before);
-        const int col = (int)readlane32((uint32_t)(mine_lane ? sel : 0), src);
+        int src, col;
+        if constexpr (kList) {
+          const int cell = (int)((readlane32(lword, (int)(kk >> 2)) >> (8u * (kk & 3u))) & 0xffu);
+          src = cell / W_;
+          col = cell - src * W_;
+        } else {
+          const uint64_t cand = ~mine & ~rev & (lane < H ? rowmask : 0ull);
+          const uint32_t pc = (uint32_t)__popcll(cand);
+          const uint32_t before = wave_excl_scan(pc);
+          const bool mine_lane = kk >= before && kk < before + pc;
+          const uint64_t who = __ballot(mine_lane);
+          src = __ffsll((unsigned long long)who) - 1;
+          // the k-th candidate of the row by a popcount bisection (a clear-lowest-bit loop cost
+          // ~2x the whole click: tools/late_diag.py)
+          const int sel = (W_ && W_ <= 32) ? select_bit32((uint32_t)cand, kk - before) : select_bit64(cand, kk - before);
+          col = (int)readlane32((uint32_t)(mine_lane ? sel : 0), src);
+        }
         if (((readlane64(zero, src) >> col) & 1ull) == 0ull) {
           if (lane == src) rev |= 1ull << col;
           revealed += 1;
+          if constexpr (kList) {  // entry kk leaves the list: the entries after it move down one
+            const uint32_t nxt = dpp32<0x130>(lword);  // lane l <- lane l + 1 (wave_shl:1)
+            const uint32_t shifted = (lword >> 8) | (nxt << 24);
+            const int lk = (int)(kk >> 2);
+            const uint32_t keep = lane < lk ? 0xffffffffu : (lane == lk ? (1u << (8u * (kk & 3u))) - 1u : 0u);
+            lword = (lword & keep) | (shifted & ~keep);
+          }
         } else {  // flood_fill_reveal (env_numba.py:17-77) from a zero cell, as board_click
           const uint64_t allow = ~mine & ~rev & (lane < H ? rowmask : 0ull);
           uint64_t Fr = (lane == src) ? (1ull << col) : 0ull;
@@ -2110,6 +2215,7 @@ __device__ __forceinline__ void late_env(const KParams& p, Pcg& L, const LateCfg
           }
           rev |= Fr;
           revealed += (int)wave_sum((uint32_t)__popcll(Fr));
+          if constexpr (kList) build_list();
         }
         step_count += 1;
         done = revealed >= safe_total;  // a win (env.py:133-140)
@@ -2163,15 +2269,16 @@ __global__ __launch_bounds__(64) void k_late(KParams p, Pcg* lstate, LateCfg lc,
   __shared__ uint32_t sTab[(H_ && W_) ? H_ * W_ : kMaxH * kMaxW];
   const int lane = lane_id();
   const Geo<H_, W_> g(p.H, p.W);
-  Pcg L;
-  L.hi = lstate->hi;
-  L.lo = lstate->lo;
-  L.ihi = lstate->ihi;
-  L.ilo = lstate->ilo;
-  L.has32 = lstate->has32;
-  L.uinteger = lstate->uinteger;
+  LateRng L;
+  L.base.hi = lstate->hi;
+  L.base.lo = lstate->lo;
+  L.base.ihi = lstate->ihi;
+  L.base.ilo = lstate->ilo;
+  L.base.has32 = lstate->has32;
+  L.base.uinteger = lstate->uinteger;
   uint64_t J[4];
   load_jump(p.jump, lane, J);
+  lr_fill(L, J);
   // the flags of 64 envs per load and ballot (one dependent scalar load per env cost ~0.5 us each);
   // the next env's state is loaded before the current env runs
   int64_t base = -kWave;
@@ -2211,11 +2318,12 @@ __global__ __launch_bounds__(64) void k_late(KParams p, Pcg* lstate, LateCfg lc,
       for (int k = 0; k < 16; ++k) p.diag[k] = dv[k];
   }
 #endif
+  const Pcg Lf = lr_state(L);
   if (lane == 0) {
-    lstate->hi = L.hi;
-    lstate->lo = L.lo;
-    lstate->has32 = L.has32;
-    lstate->uinteger = L.uinteger;
+    lstate->hi = Lf.hi;
+    lstate->lo = Lf.lo;
+    lstate->has32 = Lf.has32;
+    lstate->uinteger = Lf.uinteger;
   }
 }
 

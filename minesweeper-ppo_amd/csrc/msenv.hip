@@ -2231,6 +2231,10 @@ __device__ __forceinline__ void late_env(const KParams& p, Rng& L, const LateCfg
       step_count = 0;
     }
   }
+  if (!late) {  // no late start: board, meta and obs are what the step (or ms_reset) just wrote
+    LSTAMP(3);
+    return;
+  }
   if (lane == 0) {
     mp->st_hi = rng.hi;
     mp->st_lo = rng.lo;
@@ -2248,8 +2252,7 @@ __device__ __forceinline__ void late_env(const KParams& p, Rng& L, const LateCfg
              p.codes ? p.codes + env * A : nullptr, sR, sM, fc, g, lane, reinterpret_cast<uint8_t*>(sTab));
   }
   __syncthreads();
-  if (late) LSTAMP(9);
-  else LSTAMP(3);
+  LSTAMP(9);
 }
 
 __device__ __forceinline__ void load_jump(const uint64_t* jump, int lane, uint64_t (&J)[4]) {

@@ -50,9 +50,10 @@ VARIANT_FWD, VARIANT_BWD = 0, 1  # mc_set_variant kernels (include/msenv_debug.h
 
 
 class kernel_variant:
-    """Context manager: run mc_conv_gn_fwd (kernel 0) or mc_conv_gn_bwd (kernel 1) on one
-    variant -- 0 the dispatcher's choice, 1 the per-sample kernel, 2 the wave-specialised
-    kernel -- for parity tests of every path and same-process A/B timing."""
+    """Context manager: run mc_conv_gn_fwd (kernel 0) or mc_conv_gn_bwd (kernel 1) on one variant
+    -- 0 the dispatcher's choice, 1 the per-sample kernel, 2 / 3 the pixel-split wave-specialised
+    kernels, 4 / 5 the channel-split forward (include/msenv_debug.h) -- for parity tests of every
+    path and same-process A/B timing."""
 
     def __init__(self, kernel: int, variant: int):
         self.kernel, self.variant = kernel, variant

@@ -7,11 +7,38 @@ import argparse
 import csv
 import glob
 import os
-import sys
+import re
 from collections import defaultdict
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from ppo_pmc_summary import label  # noqa: E402  (kernel-name demangling)
+
+
+def label(name):
+    """'k_conv_gn_fwd_ws3<f16, 96, 8, true, false>' from a rocprofv3 kernel name (mangled
+    element-type templates, or demangled '(anonymous namespace)::k_...<...>(...)')."""
+    if name.startswith("_ZN12_GLOBAL__N_1"):
+        rest = name[len("_ZN12_GLOBAL__N_1"):]
+        n = int(re.match(r"(\d+)", rest).group(1))
+        d = len(str(n))
+        base, rest = rest[d:d + n], rest[d + n:]
+        args = []
+        if rest.startswith("I"):
+            i = 1
+            while i < len(rest) and rest[i] != "E":
+                if rest.startswith("DF16b", i):
+                    args.append("bf16"); i += 5
+                elif rest.startswith("DF16_", i):
+                    args.append("f16"); i += 5
+                elif rest.startswith("Lb", i):
+                    args.append("true" if rest[i + 2] == "1" else "false"); i += 4
+                elif rest.startswith("Li", i):
+                    j = rest.index("E", i)
+                    args.append(rest[i + 2:j]); i = j + 1
+                else:
+                    break
+        return f"{base}<{', '.join(args)}>" if args else base
+    short = name.split("(anonymous namespace)::", 1)[-1]
+    m = re.match(r"\w+(<[^()]*>)?", short)
+    return m.group(0) if m else short
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--pmc", required=True)

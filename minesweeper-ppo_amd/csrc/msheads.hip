@@ -384,15 +384,37 @@ __global__ __launch_bounds__(256, 2) void k_heads_bwd(HeadBwdParams<E> p) {
   }
 }
 
+// Sum of the G partials, deterministic (as k_reduce in mscnn_bwd.hip): a 256-thread block covers
+// 64 outputs with 4 slices over g (slice s sums g = s, s + 4, ... on four independent
+// accumulators, so a thread keeps four loads in flight), combined in fixed order through LDS.
+// One thread per output over all G serially kept ~74 blocks on the GPU: 123 us per call.
+constexpr int HR_S = 4, HR_IB = 256 / HR_S;
 __global__ __launch_bounds__(256) void k_heads_reduce(const float* __restrict__ part, int G, float* __restrict__ dw1,
                                                       float* __restrict__ dw2, float* __restrict__ db1) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= PART) return;
-  float s = 0.f;
-  for (int g = 0; g < G; ++g) s += part[(size_t)g * PART + i];
-  if (i < NH * C) dw1[i] = s;
-  else if (i < NH * C + NH) dw2[i - NH * C] = s;
-  else db1[i - NH * C - NH] = s;
+  __shared__ float sp[HR_S][HR_IB];
+  const int li = threadIdx.x % HR_IB, sl = threadIdx.x / HR_IB;
+  const int i = blockIdx.x * HR_IB + li;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (i < PART) {
+    int g = sl;
+    for (; g + 3 * HR_S < G; g += 4 * HR_S) {
+      a0 += part[(size_t)g * PART + i];
+      a1 += part[(size_t)(g + HR_S) * PART + i];
+      a2 += part[(size_t)(g + 2 * HR_S) * PART + i];
+      a3 += part[(size_t)(g + 3 * HR_S) * PART + i];
+    }
+    for (; g < G; g += HR_S) a0 += part[(size_t)g * PART + i];
+  }
+  sp[sl][li] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (sl == 0 && i < PART) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < HR_S; ++k) s += sp[k][li];
+    if (i < NH * C) dw1[i] = s;
+    else if (i < NH * C + NH) dw2[i - NH * C] = s;
+    else db1[i - NH * C - NH] = s;
+  }
 }
 
 int bwd_grid(int64_t M) {  // two k_heads_bwd workgroups per CU
@@ -464,8 +486,8 @@ int run_heads_bwd(const uint16_t* f, const float* dlp, const float* dlm, const u
   hipLaunchKernelGGL(k_heads_bwd<E>, dim3(grid), dim3(256), sizeof(HeadLds<E>), s, p);
   int rc = check("k_heads_bwd");
   if (rc) return rc;
-  hipLaunchKernelGGL(k_heads_reduce, dim3((PART + 255) / 256), dim3(256), 0, s, (const float*)work, grid, dw1, dw2,
-                     db1);
+  hipLaunchKernelGGL(k_heads_reduce, dim3((PART + HR_IB - 1) / HR_IB), dim3(256), 0, s, (const float*)work, grid, dw1,
+                     dw2, db1);
   return check("k_heads_reduce");
 }
 

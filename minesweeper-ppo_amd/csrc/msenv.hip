@@ -2510,16 +2510,21 @@ __device__ __forceinline__ int pk_tape_cell(uint32_t mine, uint32_t rev, int lan
 template <int H_, int W_, int WPG, int BPW>
 __global__ __launch_bounds__(64 * WPG) void k_run_packed(KParams p, RunParams rp) {
   constexpr int LPB = kWave / BPW;
+  constexpr bool BIG = packable16<H_, W_>();  // 16x16: place_packed3 + pk_emit16
   static_assert(BPW == 2 || BPW == 4, "boards per wave");
-  static_assert(packable<H_, W_>(), "packed board shape");
+  static_assert(packable<H_, W_>() || (BIG && BPW == 4), "packed board shape");
   constexpr int A = H_ * W_;
   constexpr int RPW = 64 / W_;
   constexpr int NW = (H_ + RPW - 1) / RPW;
-  __shared__ PackedLds<H_, W_, BPW> S_all[WPG];
+  using Lds = std::conditional_t<BIG, PackedLds16<H_, W_, BPW>, PackedLds<H_, W_, BPW>>;
+  __shared__ Lds S_all[WPG];
   const int lane = lane_id();
   const int r = lane & (LPB - 1);
   const int wv = (WPG == 1) ? 0 : (int)rfl(threadIdx.x >> 6);
-  PackedLds<H_, W_, BPW>& S = S_all[wv];
+  Lds& S = S_all[wv];
+  uint32_t* scr;
+  if constexpr (BIG) scr = S.scr;
+  else scr = S.row;
   const int64_t env0 = ((int64_t)blockIdx.x * WPG + wv) * BPW;
   if (env0 >= p.n) return;  // (wave-uniform)
   const int64_t env_raw = env0 + (lane / LPB);
@@ -2540,7 +2545,7 @@ __global__ __launch_bounds__(64 * WPG) void k_run_packed(KParams p, RunParams rp
     bool done, mines_changed = false, cell_rev;
     int outcome;
     uint32_t newly, total_rev;
-    pk_click<H_, W_, LPB>(p, rng, mine, rev, fc, cell, J, S.row, lane, nullptr, done, outcome, newly, total_rev,
+    pk_click<H_, W_, LPB>(p, rng, mine, rev, fc, cell, J, scr, lane, nullptr, done, outcome, newly, total_rev,
                           mines_changed, cell_rev);
     double reward = 0.0;
     if (outcome == MS_OUTCOME_LOSS) reward += p.loss_reward;
@@ -2555,9 +2560,15 @@ __global__ __launch_bounds__(64 * WPG) void k_run_packed(KParams p, RunParams rp
       fc = false;
       step_count = 0;
     }
-    if (p.obs || p.mask)
-      pk_emit<H_, W_, BPW, LPB>(p.obs ? p.obs + (sbase + env0) * 10 * A : nullptr,
-                                p.mask ? p.mask + (sbase + env0) * A : nullptr, nbl, mine, rev, fc, S, lane, nullptr);
+    if constexpr (BIG) {
+      if (p.obs || p.mask)
+        pk_emit16<H_, W_, BPW>(p.obs ? p.obs + (sbase + env0) * 10 * A : nullptr,
+                               p.mask ? p.mask + (sbase + env0) * A : nullptr, nbl, mine, rev, fc, lane);
+    } else {
+      if (p.obs || p.mask)
+        pk_emit<H_, W_, BPW, LPB>(p.obs ? p.obs + (sbase + env0) * 10 * A : nullptr,
+                                  p.mask ? p.mask + (sbase + env0) * A : nullptr, nbl, mine, rev, fc, S, lane, nullptr);
+    }
     wave_sync();  // this step's LDS reads before the next step's placement / image writes
   }
   pk_store_state<H_, W_, BPW, LPB>(p.meta + env, p.mine_words + env * NW, p.rev_words + env * NW, rng, step_count, fc,
@@ -2817,6 +2828,10 @@ bool shape_ok(const ms_cfg* c) {
 // 32k+, the one-board kernel's 4x more waves hide latency better at 4k; profiles/r04/
 // packed16_step.txt); MS_DBG_FORCE_PACKED takes the packed kernel at any count
 constexpr int64_t kPack16MinEnvs = 65536;
+// the multistep form (ms_run_tape), whose boards stay in registers across the launch's steps: the
+// packed kernel measured 3 % faster at 4,096 envs, 3-12 % at 32,768 and ~10 % at 65,536 (a wash at
+// 8,192; profiles/r04/packed16_run.txt), so it is taken at every env count
+constexpr int64_t kPack16RunMinEnvs = 0;
 
 template <int H_, int W_>
 void launch_step(const KParams& p, int epw, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
@@ -2857,6 +2872,17 @@ void launch_step(const KParams& p, int epw, hipStream_t s, hipEvent_t ev0, hipEv
 
 template <int H_, int W_>
 void launch_run(const KParams& p, const RunParams& r, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+  if constexpr (packable16<H_, W_>()) {  // (as launch_step; each step's 4-board chunk is 16-B aligned)
+    if (p.K >= 1 && p.K <= 48 &&
+        !(p.dbg_flags & (MS_DBG_ONE_BOARD_PER_WAVE | MS_DBG_FORCE_CHAIN_PLACEMENT | MS_DBG_TWO_BOARDS_PER_WAVE)) &&
+        (p.n >= kPack16RunMinEnvs || (p.dbg_flags & MS_DBG_FORCE_PACKED)) && ((uintptr_t)p.obs & 15u) == 0 &&
+        ((uintptr_t)p.mask & 3u) == 0) {
+      constexpr int WPG = 4;
+      const unsigned grid = (unsigned)((p.n + 4 * WPG - 1) / (4 * WPG));
+      hipExtLaunchKernelGGL((k_run_packed<H_, W_, WPG, 4>), dim3(grid), dim3(64 * WPG), 0, s, ev0, ev1, 0, p, r);
+      return;
+    }
+  }
   if constexpr (packable<H_, W_>()) {
     // small boards: four per wave (k_run_packed); each step's 4-board obs / mask chunk must
     // start 16-B / 4-B aligned, in every slot

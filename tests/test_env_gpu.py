@@ -432,6 +432,27 @@ def test_run_tape_packed_equals_one_board_per_wave(gpu, H, W, K, N, slots, mode)
             assert torch.equal(snaps[0][k], sn[k]), k
 
 
+@pytest.mark.parametrize("K,N,slots", [(40, 203, True), (40, 130, False), (48, 66, True)])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_run_tape_packed16_equals_one_board_per_wave(gpu, K, N, slots, mode):
+    """16x16 k_run_packed (four boards per wave, place_packed3, pk_emit16; forced below its env-count
+    threshold) is bit-exact with k_run over two launches: every output slot, boards and RNG state."""
+    from ms_amd import _lib as L
+    vs = [_vec(16, 16, K, N, seed=29) for _ in range(2)]
+    vs[0].set_debug_flags(L.MS_DBG_FORCE_PACKED)
+    vs[1].set_debug_flags(L.MS_DBG_ONE_BOARD_PER_WAVE)
+    for v in vs:
+        v.reset()
+    for t0 in (3, 40):
+        outs = [v.run_tape(t0, 30, mode, slots=slots) for v in vs]
+        for k in _RUN_KEYS:
+            assert torch.equal(outs[0][k], outs[1][k]), (t0, k)
+    assert np.array_equal(vs[0].rng_state(), vs[1].rng_state())
+    sa, sb = vs[0].snapshot_tensors(), vs[1].snapshot_tensors()
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
+
+
 def test_run_tape_sharded_and_late_start(gpu):
     from ms_amd import EnvConfig, VecMinesweeper
     from ms_amd._lib import MsEnvError

@@ -30,9 +30,14 @@ int ms_set_debug_flags(ms_handle* h, uint32_t flags);
  * conv waves + memory waves; s_barrier / LDS-counter group barriers), 4 / 5 = the forward's
  * channel-split wave-specialised kernel (3 conv waves of 32 output channels each, LDS-DMA weight
  * rings, 4 memory waves; B operands single- / double-buffered), where the board fits them
- * (P <= 256). Process-wide, not thread-safe. */
+ * (P <= 256). Kernel 2 = the weight gradient of mc_conv_gn_bwd on 16x16 boards with 96
+ * channels: variant 0 = default (= 3), 1 = k_wgrad (three ci-slice workgroups a sample group,
+ * the compiler's LDS-read schedule), 2 = k_wgrad with the next step's reads pinned between this
+ * step's MFMAs, 3 = k_wgrad_c96 (one workgroup a CU owns all 81 tiles; dy by LDS-DMA).
+ * Process-wide, not thread-safe. */
 #define MC_VAR_FWD 0
 #define MC_VAR_BWD 1
+#define MC_VAR_WGRAD 2
 int mc_set_variant(int32_t kernel, int32_t variant);
 
 /* Measurement (bench.py): while set, every k_step / k_run launch of this handle is

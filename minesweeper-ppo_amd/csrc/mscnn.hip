@@ -30,7 +30,7 @@
 namespace mc {
 
 thread_local char g_err[256] = "";
-int g_variant[MCV_COUNT] = {0, 0};
+int g_variant[MCV_COUNT] = {0, 0, 0};
 
 int num_cus() {
   static int ncu = 0;

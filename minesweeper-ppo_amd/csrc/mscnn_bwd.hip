@@ -741,7 +741,18 @@ struct WgradParams {
   const E* x;
   float* part;  // [G][9][96][CIN]
   int N, H, W, G;
+  int exp;  // MC_WSX builds: timing experiments (WGX_* bits; results wrong)
 };
+// timing experiments of k_wgrad (libmsenv_wsx.so, mc_set_wgrad_exp; tools/wgrad_exp.py): each bit
+// removes one part so its cost can be read off the launch time
+#ifdef MC_WSX
+#define WGX(bit) ((p.exp & (bit)) != 0)
+int g_wgrad_exp = 0;
+#else
+#define WGX(bit) false
+#endif
+[[maybe_unused]] constexpr int WGX_NO_STAGE = 1, WGX_NO_LOOP = 2, WGX_NO_BAR = 4, WGX_SAME_SAMPLE = 8, WGX_NO_DMA = 16,
+                               WGX_NO_XLOAD = 32;
 
 __host__ __device__ inline int wgrad_lds(int H, int W) {
   const int P = H * W, Ppad = (P + 15) & ~15;
@@ -753,7 +764,19 @@ __host__ __device__ inline int wgrad_lds(int H, int W) {
 // PF (16x16 boards, 96 channels): the next sample's dy and x slice are loaded into
 // registers (12 + 4 16-B chunks per thread) while this sample's MFMAs run, and written
 // to LDS after the trailing barrier, so the load round trip leaves the critical path.
-template <typename E, int CIN, int T0, int NT, bool PF>
+// SG: the next step's NR LDS reads spread over this step's NT MFMAs by sched_group_barrier, so
+// every MFMA's operands were read one step (NT MFMAs) earlier
+template <int NR, int NT, int T = 0>
+__device__ __forceinline__ void pin_reads_mfma() {
+  if constexpr (T < NT) {
+    constexpr int r = (NR * (T + 1)) / NT - (NR * T) / NT;
+    if constexpr (r > 0) __builtin_amdgcn_sched_group_barrier(0x100, r, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    pin_reads_mfma<NR, NT, T + 1>();
+  }
+}
+
+template <typename E, int CIN, int T0, int NT, bool PF, bool SG>
 __device__ __forceinline__ void wgrad_body(const WgradParams<E>& p, E* sDY, E* sX, int gid, int ci0) {
   typedef typename EV<E>::v8 E8;
   constexpr int TAP0 = T0 / 3, TAP1 = (T0 + NT - 1) / 3, NTAP = TAP1 - TAP0 + 1;
@@ -780,7 +803,8 @@ __device__ __forceinline__ void wgrad_body(const WgradParams<E>& p, E* sDY, E* s
   constexpr int NDY = PF ? 256 * NC8 / 256 : 1, NXS = PF ? 256 * XCH / 256 : 1;
   u32x4 rdy[NDY], rx[NXS];
   auto prefetch = [&](int n) {  // PF: P == 256, W == 16
-    if (n < p.N) {
+    if (n < p.N && !WGX(WGX_NO_STAGE)) {
+      if (WGX(WGX_SAME_SAMPLE)) n = gid;
       const u32x4* dys = reinterpret_cast<const u32x4*>(p.dy + (size_t)n * 256 * COUT);
 #pragma unroll
       for (int k = 0; k < NDY; ++k) rdy[k] = dys[tid + 256 * k];
@@ -794,6 +818,7 @@ __device__ __forceinline__ void wgrad_body(const WgradParams<E>& p, E* sDY, E* s
   if (PF) prefetch(gid);
   for (int n = gid; n < p.N; n += p.G) {
     if (PF) {
+      if (!WGX(WGX_NO_STAGE)) {
 #pragma unroll
       for (int k = 0; k < NDY; ++k) *reinterpret_cast<u32x4*>(&sDY[(tid + 256 * k) * 8]) = rdy[k];
 #pragma unroll
@@ -802,7 +827,8 @@ __device__ __forceinline__ void wgrad_body(const WgradParams<E>& p, E* sDY, E* s
         const int r = px >> 4, cc = px & 15;
         *reinterpret_cast<u32x4*>(&sX[((r + 1) * 18 + cc + 1) * 32 + kk * 8]) = rx[k];
       }
-      __syncthreads();
+      }
+      if (!WGX(WGX_NO_BAR)) __syncthreads();
       prefetch(n + p.G);
       asm volatile("" ::: "memory");  // the prefetch is issued before the MFMA loop
     } else {
@@ -818,7 +844,8 @@ __device__ __forceinline__ void wgrad_body(const WgradParams<E>& p, E* sDY, E* s
       }
       __syncthreads();
     }
-    if (PF) {
+    if (PF && WGX(WGX_NO_LOOP)) {
+    } else if (PF) {
       // 16 pixel steps, operands double-buffered: step k+1's LDS reads are issued
       // before step k's MFMAs
       auto ld = [&](int k0, E8 (&a)[3], E8 (&b)[NTAP]) {
@@ -841,13 +868,22 @@ __device__ __forceinline__ void wgrad_body(const WgradParams<E>& p, E* sDY, E* s
         }
       };
       E8 a0[3], b0[NTAP], a1[3], b1[NTAP];
+      constexpr int NR = 6 + 2 * NTAP;
       ld(0, a0, b0);
+      if constexpr (SG) __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
 #pragma unroll
       for (int k0 = 0; k0 < 256; k0 += 32) {
         ld(k0 + 16, a1, b1);
         mm(a0, b0);
-        if (k0 + 32 < 256) ld(k0 + 32, a0, b0);
-        mm(a1, b1);
+        if constexpr (SG) pin_reads_mfma<NR, NT>();
+        if (k0 + 32 < 256) {
+          ld(k0 + 32, a0, b0);
+          mm(a1, b1);
+          if constexpr (SG) pin_reads_mfma<NR, NT>();
+        } else {
+          mm(a1, b1);
+          if constexpr (SG) pin_reads_mfma<0, NT>();
+        }
       }
     } else
     for (int k0 = 0; k0 < Ppad; k0 += 16) {
@@ -874,7 +910,7 @@ __device__ __forceinline__ void wgrad_body(const WgradParams<E>& p, E* sDY, E* s
         acc[t] = mfma32(a[tt % 3], b[tt / 3 - TAP0], acc[t]);
       }
     }
-    __syncthreads();
+    if (!WGX(WGX_NO_BAR)) __syncthreads();
   }
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
@@ -890,7 +926,7 @@ __device__ __forceinline__ void wgrad_body(const WgradParams<E>& p, E* sDY, E* s
   }
 }
 
-template <typename E, int CIN, bool PF>
+template <typename E, int CIN, bool PF, bool SG>
 __global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams<E> p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NCI = CIN / 32 > 0 ? CIN / 32 : 1;
@@ -906,10 +942,174 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams<E> p) {
   const int cig = j % NCI, gid = (j / NCI) * 8 + xcd;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   switch (wave) {
-    case 0: wgrad_body<E, CIN, 0, 7, PF>(p, sDY, sX, gid, cig * 32); break;
-    case 1: wgrad_body<E, CIN, 7, 7, PF>(p, sDY, sX, gid, cig * 32); break;
-    case 2: wgrad_body<E, CIN, 14, 7, PF>(p, sDY, sX, gid, cig * 32); break;
-    default: wgrad_body<E, CIN, 21, 6, PF>(p, sDY, sX, gid, cig * 32); break;
+    case 0: wgrad_body<E, CIN, 0, 7, PF, SG>(p, sDY, sX, gid, cig * 32); break;
+    case 1: wgrad_body<E, CIN, 7, 7, PF, SG>(p, sDY, sX, gid, cig * 32); break;
+    case 2: wgrad_body<E, CIN, 14, 7, PF, SG>(p, sDY, sX, gid, cig * 32); break;
+    default: wgrad_body<E, CIN, 21, 6, PF, SG>(p, sDY, sX, gid, cig * 32); break;
+  }
+}
+
+// k_wgrad_c96 (16x16 boards, 96 -> 96 channels; mc_set_variant(MC_VAR_WGRAD, 3)): one 512-thread
+// workgroup per CU owns all 81 (tap, co tile, ci tile) 32x32 tiles, so a sample's dy and x cross
+// HBM and LDS once (k_wgrad's three ci-slice workgroups read dy three times and write 192 KB of
+// LDS per sample; this one 48 KB of x, and its dy arrives by LDS-DMA, double-buffered, while the
+// previous sample's MFMAs run). Wave w owns tap w for every (co tile, ci tile) -- 9 tiles, B
+// operands x[tap w][ci tile 0..2] -- plus one or two tiles of tap 8 (ci tile m(w)); 21/20/20/20
+// tiles per SIMD. Partials [G][9][96][96] as k_wgrad's, same k_reduce.
+constexpr int WC_DY = 256 * COUT;       // elements of one dy buffer
+constexpr int WC_SX = 18 * 18 * COUT;   // zero-halo x image, 96 channels a pixel
+constexpr int WC_LDS = (2 * WC_DY + WC_SX) * 2;  // 160,512 B
+static_assert(WC_LDS <= 160 * 1024, "k_wgrad_c96 LDS");
+
+// One full-wave LDS-DMA of 1 KiB (16 B a lane, lane-linear at LDS byte address m0v) issued from
+// inline asm: as a builtin, the compiler makes every later LDS read wait for it (vmcnt(0) in
+// front of the MFMA loop, the prefetch serialised); the kernel waits for it explicitly
+__device__ __forceinline__ void dma16_asm(const void* src, uint32_t m0v) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0v) : "memory", "m0");
+}
+
+template <int WV>
+struct WgcTiles {
+  static constexpr int NT = WV == 0 ? 11 : 10;        // tiles
+  static constexpr int M8 = WV <= 1 ? 0 : (WV <= 4 ? 1 : 2);  // ci tile of this wave's tap-8 tiles
+  static constexpr int co(int t) { return t < 9 ? t % 3 : (WV == 0 ? t - 9 : (WV == 1 ? 2 : (WV - 2) % 3)); }
+  static constexpr int b(int t) { return t < 9 ? t / 3 : 3; }  // B operand: 0..2 tap WV ci tile b, 3 tap 8
+  static constexpr int tap(int bi) { return bi < 3 ? WV : 8; }
+  static constexpr int cis(int bi) { return bi < 3 ? bi : M8; }
+};
+
+template <typename E, int WV>
+__device__ __forceinline__ void wgc_body(const WgradParams<E>& p, E* sDY, E* sX, int gid) {
+  typedef typename EV<E>::v8 E8;
+  using T = WgcTiles<WV>;
+  constexpr int NT = T::NT;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int col = 16 * (g & 1) + 4 * pp;  // tr-read column of this lane within a 32-wide block
+  const int rowoff = 8 * (g >> 1) + q;    // tr-read pixel offset within a 16-deep k step
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+  u32x4 rx[6];
+  // sample n's dy -> sDY[buf] by LDS-DMA (this wave's 6 KiB: six full-wave 1-KiB instructions,
+  // lane-linear destinations) and its x -> registers (6 16-B chunks a thread)
+  auto issue = [&](int n, int buf) {
+    if (n < p.N && !WGX(WGX_NO_STAGE)) {
+      const E* src = p.dy + (size_t)n * WC_DY;
+      const int ln = lane + opaque0();
+      const uint32_t dst = (uint32_t)(size_t)((__attribute__((address_space(3))) E*)(sDY + buf * WC_DY)) + WV * 6 * 1024;
+      if (!WGX(WGX_NO_DMA)) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) dma16_asm(src + ((WV * 6 + k) * 64 + ln) * 8, dst + k * 1024);
+      }
+      if (!WGX(WGX_NO_XLOAD)) {
+        const u32x4* xs = reinterpret_cast<const u32x4*>(p.x + (size_t)(WGX(WGX_SAME_SAMPLE) ? gid : n) * WC_DY);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) rx[k] = xs[tid + 512 * k];
+      }
+    }
+  };
+  auto put_x = [&]() {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const int c = tid + 512 * k, px = c / 12, kk = c - px * 12;
+      *reinterpret_cast<u32x4*>(&sX[(((px >> 4) + 1) * 18 + (px & 15) + 1) * COUT + kk * 8]) = rx[k];
+    }
+  };
+  int buf = 0;
+  issue(gid, 0);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (a builtin, so that the compiler's own count sees it)
+  put_x();
+  __syncthreads();
+  for (int n = gid; n < p.N; n += p.G, buf ^= 1) {
+    issue(n + p.G, buf ^ 1);
+    asm volatile("" ::: "memory");  // the prefetch is issued before the MFMA loop
+    const E* D = sDY + buf * WC_DY;
+    auto ld = [&](int k0, E8 (&a)[3], E8 (&b)[4]) {
+#pragma unroll
+      for (int cot = 0; cot < 3; ++cot) {
+        const E* base = D + (k0 + rowoff) * COUT + cot * 32 + col;
+        a[cot] = cat8(lds_tr4(base), lds_tr4(base + 4 * COUT));
+      }
+      const int px0 = k0 + rowoff, px1 = px0 + 4;
+      const int h0 = ((px0 >> 4) + 1) * 18 + (px0 & 15) + 1, h1 = ((px1 >> 4) + 1) * 18 + (px1 & 15) + 1;
+#pragma unroll
+      for (int bi = 0; bi < 4; ++bi) {
+        const int tap = T::tap(bi), toff = ((tap / 3 - 1) * 18 + (tap % 3 - 1)) * COUT + T::cis(bi) * 32 + col;
+        b[bi] = cat8(lds_tr4(sX + h0 * COUT + toff), lds_tr4(sX + h1 * COUT + toff));
+      }
+    };
+    auto mm = [&](const E8 (&a)[3], const E8 (&b)[4]) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = mfma32(a[T::co(t)], b[T::b(t)], acc[t]);
+    };
+    if (WGX(WGX_NO_LOOP)) {
+    } else if constexpr (NT == 10) {
+      // operands double-buffered: step k+1's 14 reads spread between step k's MFMAs
+      E8 a0[3], b0[4], a1[3], b1[4];
+      ld(0, a0, b0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 14, 0);
+#pragma unroll
+      for (int k0 = 0; k0 < 256; k0 += 32) {
+        ld(k0 + 16, a1, b1);
+        mm(a0, b0);
+        pin_reads_mfma<14, NT>();
+        if (k0 + 32 < 256) {
+          ld(k0 + 32, a0, b0);
+          mm(a1, b1);
+          pin_reads_mfma<14, NT>();
+        } else {
+          mm(a1, b1);
+          pin_reads_mfma<0, NT>();
+        }
+      }
+    } else {
+      // wave 0 (11 tiles): one step's operands live at a time (176 accumulators and the x
+      // prefetch leave no room for two); its SIMD partner covers the read latency
+#pragma unroll
+      for (int k0 = 0; k0 < 256; k0 += 16) {
+        E8 a[3], b[4];
+        ld(k0, a, b);
+        mm(a, b);
+        __builtin_amdgcn_sched_group_barrier(0x100, 14, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, NT, 0);
+      }
+    }
+    __syncthreads();  // sX and sDY[buf] are free
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMA and x loads have landed
+    if (n + p.G < p.N && !WGX(WGX_NO_STAGE) && !WGX(WGX_NO_XLOAD)) put_x();
+    __syncthreads();  // sX and sDY[buf ^ 1] (every wave's DMA) complete
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int tap = T::tap(T::b(t)), ci = T::cis(T::b(t)) * 32 + (lane & 31), cot = T::co(t);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = cot * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      p.part[(((size_t)gid * 9 + tap) * COUT + co) * 96 + ci] = acc[t][r];
+    }
+  }
+}
+
+template <typename E>
+__global__ __launch_bounds__(512, 1) void k_wgrad_c96(WgradParams<E> p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  E* sDY = reinterpret_cast<E*>(smem);  // [2][256][96]
+  E* sX = sDY + 2 * WC_DY;              // [18 * 18][96], zero halo
+  for (int i = threadIdx.x; i < WC_SX / 8; i += 512) *reinterpret_cast<u32x4*>(&sX[i * 8]) = u32x4{0u, 0u, 0u, 0u};
+  __syncthreads();
+  const int gid = blockIdx.x;
+  switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
+    case 0: wgc_body<E, 0>(p, sDY, sX, gid); break;
+    case 1: wgc_body<E, 1>(p, sDY, sX, gid); break;
+    case 2: wgc_body<E, 2>(p, sDY, sX, gid); break;
+    case 3: wgc_body<E, 3>(p, sDY, sX, gid); break;
+    case 4: wgc_body<E, 4>(p, sDY, sX, gid); break;
+    case 5: wgc_body<E, 5>(p, sDY, sX, gid); break;
+    case 6: wgc_body<E, 6>(p, sDY, sX, gid); break;
+    default: wgc_body<E, 7>(p, sDY, sX, gid); break;
   }
 }
 
@@ -951,6 +1151,7 @@ void launch_reduce(const float* part, int G, int64_t n, float* out, hipStream_t 
 
 // ------------------------------------------------------------------------------------
 struct Plan {
+  bool c96 = false;  // k_wgrad_c96 (16x16 boards, 96 channels; the default there)
   int grid_d, grid_w, G;
   int64_t gn_part, w_part;
 };
@@ -964,10 +1165,15 @@ Plan make_plan(int n, int h, int w, int cin) {
   if (J < 1) J = 1;
   pl.G = 8 * J;
   pl.grid_w = 8 * nci * J;
+  int gmax = pl.G;
+  // 16x16 boards, 96 channels, variant 3: k_wgrad_c96, one workgroup (partial row) per CU
+  if (cin == 96 && h == 16 && w == 16) {
+    if (ncu > gmax) gmax = ncu;
+    pl.c96 = g_variant[MCV_WGRAD] == 0 || g_variant[MCV_WGRAD] == 3;
+    if (pl.c96) pl.G = pl.grid_w = n < ncu ? n : ncu;
+  }
   pl.gn_part = (int64_t)pl.grid_d * 3 * COUT;
-  pl.w_part = (int64_t)pl.G * 9 * COUT * cin;
-  (void)h;
-  (void)w;
+  pl.w_part = (int64_t)gmax * 9 * COUT * cin;  // the same workspace whichever k_wgrad runs
   return pl;
 }
 
@@ -1035,23 +1241,26 @@ int dispatch_bwd_data(const BwdDataParams<E>& p, int& grid, hipStream_t s) {
   return MS_OK;
 }
 
-template <typename E, int CIN, bool PF>
+template <typename E, int CIN, bool PF, bool SG>
 void launch_wgrad_t(const WgradParams<E>& p, int grid, size_t lds, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    set_lds_attr(k_wgrad<E, CIN, PF>);
+    set_lds_attr(k_wgrad<E, CIN, PF, SG>);
     attr = true;
   }
-  hipLaunchKernelGGL((k_wgrad<E, CIN, PF>), dim3(grid), dim3(256), lds, s, p);
+  hipLaunchKernelGGL((k_wgrad<E, CIN, PF, SG>), dim3(grid), dim3(256), lds, s, p);
 }
 
 template <typename E, int CIN>
 void launch_wgrad(const WgradParams<E>& p, int grid, size_t lds, hipStream_t s) {
   // 16x16 boards with 96 channels: the register prefetch of the next sample's dy and x slice
   if constexpr (CIN == 96) {
-    if (p.H == 16 && p.W == 16) return launch_wgrad_t<E, CIN, true>(p, grid, lds, s);
+    if (p.H == 16 && p.W == 16) {
+      if (g_variant[MCV_WGRAD] == 2) return launch_wgrad_t<E, CIN, true, true>(p, grid, lds, s);
+      return launch_wgrad_t<E, CIN, true, false>(p, grid, lds, s);
+    }
   }
-  launch_wgrad_t<E, CIN, false>(p, grid, lds, s);
+  launch_wgrad_t<E, CIN, false, false>(p, grid, lds, s);
 }
 
 int check_launch(const char* what) {
@@ -1101,8 +1310,20 @@ int run_bwd(const uint16_t* dout, const uint16_t* out, const uint8_t* relu_mask,
   wp.H = h;
   wp.W = w_;
   wp.G = pl.G;
+#ifdef MC_WSX
+  wp.exp = g_wgrad_exp;
+#else
+  wp.exp = 0;
+#endif
   const size_t lds = (size_t)wgrad_lds(h, w_);
-  if (cin == 96) launch_wgrad<E, 96>(wp, pl.grid_w, lds, s);
+  if (pl.c96) {
+    static bool attr = false;
+    if (!attr) {
+      set_lds_attr(k_wgrad_c96<E>);
+      attr = true;
+    }
+    hipLaunchKernelGGL(k_wgrad_c96<E>, dim3(pl.grid_w), dim3(512), (size_t)WC_LDS, s, wp);
+  } else if (cin == 96) launch_wgrad<E, 96>(wp, pl.grid_w, lds, s);
   else launch_wgrad<E, 16>(wp, pl.grid_w, lds, s);
   if ((rc = check_launch("k_wgrad"))) return rc;
   const int64_t nw = (int64_t)9 * COUT * cin;
@@ -1113,6 +1334,11 @@ int run_bwd(const uint16_t* dout, const uint16_t* out, const uint8_t* relu_mask,
 }  // namespace
 
 extern "C" {
+
+#ifdef MC_WSX
+// timing experiments only (tools/wgrad_exp.py): WGX_* bits of the next k_wgrad launches
+void mc_set_wgrad_exp(int32_t e) { g_wgrad_exp = e; }
+#endif
 
 int64_t mc_conv_gn_bwd_workspace(int32_t n, int32_t h, int32_t w_, int32_t cin) {
   if (n <= 0 || h <= 0 || w_ <= 0 || (cin != 16 && cin != 96)) return -1;

@@ -46,7 +46,7 @@ def _check(rc):
         raise L.MsEnvError(lib.mc_last_error().decode(errors="replace"))
 
 
-VARIANT_FWD, VARIANT_BWD = 0, 1  # mc_set_variant kernels (include/msenv_debug.h)
+VARIANT_FWD, VARIANT_BWD, VARIANT_WGRAD = 0, 1, 2  # mc_set_variant kernels (include/msenv_debug.h)
 
 
 class kernel_variant:

@@ -132,7 +132,8 @@ def test_conv_gn_bwd_matches_torch(gpu, H, W, cin, n, with_res, dt):
     storage of dy / dz / dx is 2^-9 relative; all sums are f32).
     Loose check: a full fp32 recompute from x, relative L2 <= 6e-2 (ReLU-mask flips
     where z ~ 0 between bf16 and fp32 activations dominate)."""
-    from ms_amd.fused import VARIANT_BWD, conv_gn_bwd, conv_gn_fwd, dw_to_conv, kernel_variant, prep_weight, prep_weight_t
+    from ms_amd.fused import (VARIANT_BWD, VARIANT_WGRAD, conv_gn_bwd, conv_gn_fwd, dw_to_conv, kernel_variant,
+                              prep_weight, prep_weight_t)
     torch.manual_seed(1)
     P = H * W
     x = (torch.randn(n, P, cin, device=gpu) * (0.5 if cin == 96 else 1.0)).to(dt)
@@ -165,6 +166,22 @@ def test_conv_gn_bwd_matches_torch(gpu, H, W, cin, n, with_res, dt):
                                   rmask=rm)
             for a_, b_ in zip(got, ref_rm):
                 assert (a_ is None and b_ is None) or _rel(a_, b_) < 2e-3, ws
+    if cin == 96 and (H, W) == (16, 16):
+        # k_wgrad (three ci-slice workgroups a sample group; compiler's / pinned LDS-read schedule):
+        # the same products as k_wgrad_c96 summed in another order
+        dws = []
+        for wv in (1, 2):
+            with kernel_variant(VARIANT_WGRAD, wv):
+                got = conv_gn_bwd(dout, None, y, st, g, x, H, W, wT=wT, dmask=dmask, addend=add, want_dz=with_res,
+                                  rmask=rm)
+            assert _rel(got[2], dw) < 1e-5, wv
+            dws.append(got[2])
+        assert torch.equal(dws[0], dws[1])
+        with kernel_variant(VARIANT_WGRAD, 3):  # k_wgrad_c96 (the default here) by name
+            got = conv_gn_bwd(dout, None, y, st, g, x, H, W, wT=wT, dmask=dmask, addend=add, want_dz=with_res,
+                              rmask=rm)
+        for a_, b_ in zip(got, (dx, dz, dw, dgn)):
+            assert (a_ is None and b_ is None) or torch.equal(a_, b_)
     nchw = lambda t, c: t.float().view(n, H, W, c).permute(0, 3, 1, 2).contiguous()  # noqa: E731
     nhwc = lambda t: t.permute(0, 2, 3, 1).reshape(n, P, -1)  # noqa: E731
     xr = nchw(x, cin)

@@ -42,7 +42,7 @@ def label(name):
 
 
 def layer96(lab):
-    """the 96 -> 96 layers: forward / wgrad instantiated for 96 input channels, k_bwd_data's
+    """the 96 -> 96 layers: forward / wgrad instantiated for 96 input channels (k_wgrad_c96 always), k_bwd_data's
     data-gradient variant (template argument DGRAD = true; the stem's has no dgrad)"""
     m = re.match(r"(\w+)<(.*)>$", lab)
     if not m:
@@ -50,6 +50,8 @@ def layer96(lab):
     args = [a.strip() for a in m.group(2).split(",") if a.strip() not in ("bf16", "f16")]
     if m.group(1) in ("k_conv_gn_fwd", "k_wgrad"):
         return args[0] == "96"
+    if m.group(1) == "k_wgrad_c96":  # 96 channels only
+        return True
     return m.group(1) == "k_bwd_data" and args[1] == "true"
 
 ap = argparse.ArgumentParser()

@@ -75,7 +75,7 @@ def parse():
     ap.add_argument("--env-debug-flags", type=int, default=0,
                     help="diagnostic A/B only: msenv_debug.h MS_DBG_* flags of the env handles (4: no lane packing)")
     ap.add_argument("--graph", type=int, default=1, help="capture the timed steps in a HIP graph")
-    ap.add_argument("--ppo-updates", type=int, default=2,
+    ap.add_argument("--ppo-updates", type=int, default=6,
                     help="timed combined rollout+GAE+PPO updates (0 disables; +1 untimed warm-up)")
     ap.add_argument("--ppo-steps-per-env", type=int, default=64)
     ap.add_argument("--amp", default="fp16", choices=["bf16", "fp16", "fp32"],
@@ -287,18 +287,22 @@ def ppo_bench(args, world, rank, local_rank, dev):
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    prof = []
+    prof, per_update = [], []
     for u in range(args.ppo_updates):
+        tu = time.perf_counter()
         prof.append(tr.update(1 + u, profile=True))
+        torch.cuda.synchronize()  # per-update wall time (the update ends in host reads anyway)
+        per_update.append(time.perf_counter() - tu)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el] + per_update, dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t[0])
+        el, per_update = float(t[0]), [float(v) for v in t[1:]]
     spu = el / args.ppo_updates
+    med = float(np.median(per_update))
     n_mb = cfg.ppo_epochs * cfg.mini_batches
     comm = {"allreduce": None, "note": "world 1: no collective"}
     if world > 1:
@@ -327,6 +331,11 @@ def ppo_bench(args, world, rank, local_rank, dev):
     dom = max((k for k in (kprof or {}) if k != "source"), key=lambda k: kprof[k]["mean_us"], default=None)
     return {"metric": "PPO updates/sec (combined rollout + GAE + 3x8 minibatch update)",
             "updates_per_s": 1.0 / spu, "s_per_update": spu,
+            # the spread over the timed updates (each timed alone, max over ranks), so that a change of
+            # a few per cent can be told from box-to-box noise
+            "updates": args.ppo_updates, "s_per_update_median": med,
+            "s_per_update_spread": (max(per_update) - min(per_update)) / med,
+            "s_per_update_each": [round(v, 4) for v in per_update],
             "samples_per_s": n_loc * world * T / spu, "envs_total": n_loc * world, "steps_per_env": T,
             "rollout_s": mean("rollout_s"), "gae_s": mean("gae_s"), "ppo_s": mean("ppo_s"),
             # the reference's rollout timing buckets (train_rl.py:278-288), GPU time per update

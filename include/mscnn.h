@@ -76,6 +76,63 @@ int mc_conv_gn_bwd(const uint16_t* dout, const uint16_t* out, const uint8_t* rel
 /* f32 elements of scratch mc_conv_gn_bwd needs for these sizes. */
 int64_t mc_conv_gn_bwd_workspace(int32_t n, int32_t h, int32_t w_, int32_t cin);
 
+/* Weight gradient alone (mc_conv_gn_bwd's second half): dw f32 [9][96][cin] (tap, co, ci) =
+ * sum over samples and pixels of dy[n][p][co] * x[n][p + shift(tap)][ci]. work: at least
+ * mc_conv_gn_bwd_workspace(n, h, w_, cin) floats. Deterministic (fixed-order partial sums). */
+int mc_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* work, int64_t work_floats, int32_t n,
+                  int32_t h, int32_t w_, int32_t cin, int32_t dtype, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * The whole residual stack in one launch per direction (csrc/mscnn_trunk.hip). Replaces,
+ * for `blocks` residual blocks of 96 channels (cnn_residual.py:7-27, 55-56), the per-layer
+ * launches above: a sample's activations stay in the workgroup's LDS from layer to layer,
+ * and only what the backward or the caller needs is written to HBM. Outputs are bitwise
+ * those of the per-layer entry points on the same inputs. Boards of at most 512 cells.
+ *
+ * Forward: layers[0 .. 2*blocks-1] in execution order (conv1, conv2 of block 0, ...); x0
+ * (16-bit [N][P][96]) is block 0's input. Per layer (host array of device pointers):
+ *   w       16-bit [9][96][96] (tap, co, ci), as mc_conv_gn_fwd's;
+ *   bias, gamma, beta f32 [96];
+ *   dmask   f32 [N][96] Dropout2d scale after the ReLU (conv1 layers only) or NULL;
+ *   out, ysave (16-bit [N][P][96]), stats (f32 [N][6][2]), relu_mask (u8 [N][P][12]):
+ *           as mc_conv_gn_fwd's, each may be NULL except the last layer's out.
+ * work: mc_trunk_fwd_workspace(n, h, w_) bytes, needed when a block output (the out of a
+ * conv2 layer other than the last) is NULL: it then waits there as the next block's residual. */
+#define MC_TRUNK_MAX_LAYERS 16
+typedef struct mc_fwd_layer {
+  const uint16_t* w;
+  const float* bias;
+  const float* gamma;
+  const float* beta;
+  const float* dmask;
+  uint16_t* out;
+  uint16_t* ysave;
+  float* stats;
+  uint8_t* relu_mask;
+} mc_fwd_layer;
+int64_t mc_trunk_fwd_workspace(int32_t n, int32_t h, int32_t w_);
+int mc_trunk_fwd(const uint16_t* x0, const mc_fwd_layer* layers, int32_t nlayers, void* work, int64_t work_bytes,
+                 int32_t n, int32_t h, int32_t w_, float eps, int32_t dtype, void* stream);
+
+/* Backward of the stem's GroupNorm + the residual stack: layers[0] = the stem (no input
+ * gradient: wT NULL), layers[2b+1] / [2b+2] = conv1 / conv2 of block b (wT = the 16-bit
+ * [9][96 ci][96 co] dgrad operand). Per layer the forward's ysave, stats, relu_mask, its
+ * gamma and dmask (or NULL); dy (16-bit [N][P][96], out) receives dL/dy for mc_conv_wgrad.
+ * dout = dL/d(out of the last layer). dgn (f32 [nlayers][3][96], out) = d gamma, d beta,
+ * d bias per layer. work: mc_trunk_bwd_workspace(nlayers, n, h, w_) bytes. */
+typedef struct mc_bwd_layer {
+  const uint16_t* ysave;
+  const float* stats;
+  const float* gamma;
+  const uint8_t* relu_mask;
+  const float* dmask;
+  const uint16_t* wT;
+  uint16_t* dy;
+} mc_bwd_layer;
+int64_t mc_trunk_bwd_workspace(int32_t nlayers, int32_t n, int32_t h, int32_t w_);
+int mc_trunk_bwd(const uint16_t* dout, const mc_bwd_layer* layers, int32_t nlayers, float* dgn, void* work,
+                 int64_t work_bytes, int32_t n, int32_t h, int32_t w_, int32_t dtype, void* stream);
+
 /* Policy + belief heads (cnn_residual.py:57-64, 85-96): per head
  *   logit[m] = w2 . relu(W1 f[m] + b1) + b2      over rows m of f (bf16 [M][96], NHWC trunk features).
  * w1: bf16 [nh*96][96] (policy rows first, then mine), b1/w2: f32 [nh*96], b2: f32 [nh].

@@ -19,21 +19,19 @@ extern "C" {
 #define MS_DBG_ONE_BOARD_PER_WAVE 4u     /* ms_step: k_step (one board per wave) even where the
                                             lane-packed k_step_packed applies (9x9, 8x8, K<=16) */
 #define MS_DBG_TWO_BOARDS_PER_WAVE 8u    /* k_step_packed with two boards per wave (32-lane groups) */
-#define MS_DBG_FORCE_PACKED 16u          /* 16x16: k_step_packed at any env count (default: >= 16384) */
+#define MS_DBG_FORCE_PACKED 16u          /* 16x16: k_step_packed at any env count (default: >= 65536) */
 
 int ms_set_debug_flags(ms_handle* h, uint32_t flags);
 
 /* Kernel variants of the fused CNN layer (mscnn.h), for same-process A/B runs and for the
- * parity tests of every path: kernel 0 = mc_conv_gn_fwd, 1 = mc_conv_gn_bwd; variant 0 =
- * the dispatcher's choice (default), 1 = the per-sample kernel (two 256-thread workgroups
- * per CU), 2 / 3 = the pixel-split wave-specialised kernel (one 512-thread workgroup per CU:
- * conv waves + memory waves; s_barrier / LDS-counter group barriers), 4 / 5 = the forward's
- * channel-split wave-specialised kernel (3 conv waves of 32 output channels each, LDS-DMA weight
- * rings, 4 memory waves; B operands single- / double-buffered), where the board fits them
- * (P <= 256). Kernel 2 = the weight gradient of mc_conv_gn_bwd on 16x16 boards with 96
- * channels: variant 0 = default (= 3), 1 = k_wgrad (three ci-slice workgroups a sample group,
- * the compiler's LDS-read schedule), 2 = k_wgrad with the next step's reads pinned between this
- * step's MFMAs, 3 = k_wgrad_c96 (one workgroup a CU owns all 81 tiles; dy by LDS-DMA).
+ * parity tests of every path. Kernel 0 = mc_conv_gn_fwd, 1 = mc_conv_gn_bwd's data backward:
+ * variant 0 = the dispatcher's choice (default) = 1 = the per-sample kernel (two 256-thread
+ * workgroups per CU). (Round 4's wave-specialised forms, variants 2-5, measured slower and were
+ * removed from the library in round 5; DESIGN.md §5 keeps their record, git history the code.)
+ * Kernel 2 = the weight gradient on 16x16 boards with 96 channels: variant 0 = default (= 3),
+ * 1 = k_wgrad (three ci-slice workgroups a sample group, the compiler's LDS-read schedule),
+ * 2 = k_wgrad with the next step's reads pinned between this step's MFMAs, 3 = k_wgrad_c96 (one
+ * workgroup a CU owns all 81 tiles; dy by LDS-DMA). Any other (kernel, variant) is MS_EINVAL.
  * Process-wide, not thread-safe. */
 #define MC_VAR_FWD 0
 #define MC_VAR_BWD 1

@@ -65,6 +65,9 @@ __host__ __device__ inline int bwd_data_lds(int P) { return dtile_bytes(P) + red
 // RM: the ReLU decisions come from the forward's bitmask (p.rmask), else from out
 template <typename E, int NPT, bool DGRAD, int NCH, bool RM>
 __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParams<E> p) {
+  // no contraction: every expression rounds the same way in the per-layer and the one-launch
+  // kernels (explicit fmaf where a fused multiply-add is wanted), so they agree bitwise
+#pragma clang fp contract(off)
   typedef typename EV<E>::v8 E8;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int H = p.H, W = p.W, P = H * W;
@@ -149,7 +152,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
             const float zf = (float)z8[j];
             const float yh = ((float)y8[j] - mean) * rstd;
             s1[j] += zf;
-            s2[j] += zf * yh;
+            s2[j] = __builtin_fmaf(zf, yh, s2[j]);
             s3[j] += yh;
           }
           *reinterpret_cast<u32x4*>(&sD[px * DCP + c8 * 8]) = __builtin_bit_cast(u32x4, z8);
@@ -237,7 +240,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
           const E8 y8 = __builtin_bit_cast(E8, yr[i]);
           E8 d8;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) d8[j] = (E)(A[j] * (float)z8[j] + Bg * (float)y8[j] + Cg);
+          for (int j = 0; j < 8; ++j) d8[j] = (E)__builtin_fmaf(A[j], (float)z8[j], __builtin_fmaf(Bg, (float)y8[j], Cg));
           const u32x4 v = __builtin_bit_cast(u32x4, d8);
           *reinterpret_cast<u32x4*>(&sD[px * DCP + c8 * 8]) = v;
           *reinterpret_cast<u32x4*>(&p.dy[((size_t)n * P + px) * COUT + c8 * 8]) = v;
@@ -356,381 +359,6 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
     p.part[((size_t)blockIdx.x * 3 + 0) * COUT + tid] = acc_g;
     p.part[((size_t)blockIdx.x * 3 + 1) * COUT + tid] = acc_b;
     p.part[((size_t)blockIdx.x * 3 + 2) * COUT + tid] = acc_bias;
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// Wave-specialised data backward (cin = 96, P <= 256, ReLU bitmask given): ONE 512-thread
-// workgroup per CU, the forward's split (mscnn.hip k_conv_gn_fwd_ws):
-//   waves 0-3, the dgrad waves: dx(it) = sum_tap shift(dy(it)) . W^T[tap] on the MFMA, transposed
-//     (D[ci][px]: a lane holds one pixel, four consecutive channels per register quad), W^T taps
-//     streamed through a two-slot LDS ring; dx staged over dy(it) for coalesced stores;
-//   waves 4-7, the memory waves: the dx (+ addend) stores of sample it-1, then the GroupNorm
-//     backward of sample it+1 into the other region (pass 1: dz and the channel sums, folded
-//     over two segments; reduction; coefficients; pass 2: dy into LDS and HBM, dz to HBM).
-// Sample s lives in region s & 1. Every wave passes 10 barriers per iteration (loop top, 8
-// between taps, 1 before the dx staging). The memory waves issue sample it+1's pass-1 loads
-// right after the dx stores (segment 0) and use them two segments later; the addend of sample
-// it takes the dout registers after pass 1 (a whole-iteration prefetch of dout, y and the
-// addend would need ~180 VGPRs beside the sums and spill).
-constexpr int WSB_FOLD = 11;  // the 21 pixel groups' channel sums folded into 11 LDS slots
-
-__host__ __device__ inline size_t wsb_lds_bytes(int P) {
-  return (size_t)2 * dtile_bytes(P) + (size_t)2 * COUT * DCP * 2 + (size_t)WSB_FOLD * 3 * COUT * 4 +
-         (size_t)5 * COUT * 4 + 16;  // + the grp_bar counters
-}
-
-// GB: one s_barrier per iteration (the roles' hand-off), the rest of each role's syncs by its own
-// LDS-counter barrier (grp_bar); without GB every wave passes all 10 s_barriers.
-template <typename E, int NPT, bool FULL, bool GB>
-__global__ __launch_bounds__(512, 1) void k_bwd_data_ws(BwdDataParams<E> p) {
-  typedef typename EV<E>::v8 E8;
-  typedef typename EV<E>::v4 E4;
-  constexpr int NCH = NPT == 2 ? 13 : 7;           // pixels per memory thread: px = pg + 21 i
-  constexpr int NWC = (COUT * NC8 + 255) / 256;   // 16-B chunks of one W^T tap per dgrad thread
-  constexpr int KS = COUT / 16;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int H = p.H, W = p.W, P = H * W;
-  const int RE = dtile_bytes(P) / 2;  // region elements: [P+1][DCP], row P zero
-  E* sReg = reinterpret_cast<E*>(smem);
-  E* sRing = sReg + 2 * RE;                                              // [2][ci][DCP]
-  float* sRed = reinterpret_cast<float*>(sRing + 2 * COUT * DCP);        // [WSB_FOLD][3][COUT]
-  float* sTmp = sRed + WSB_FOLD * 3 * COUT;                              // [2][COUT]
-  float* sCo = sTmp + 2 * COUT;                                          // [3][COUT]
-  unsigned* sCnt = reinterpret_cast<unsigned*>(sCo + 3 * COUT);          // dgrad | memory grp_bar counters
-  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int lane = threadIdx.x & 63;
-  const int G = gridDim.x;
-  const int cnt = p.N > (int)blockIdx.x ? (p.N - 1 - (int)blockIdx.x) / G + 1 : 0;
-
-  if (wave < WAVES) {
-    // =============================== dgrad waves ===============================
-    const int ctid = threadIdx.x, l32 = lane & 31, hh = lane >> 5;
-    // W^T taps prefetched WPF taps ahead (as the forward's conv waves: their loads queue behind
-    // the memory waves' HBM streams in the CU's vector-memory path)
-    constexpr int WPF = 3;
-    u32x4 wr[WPF][NWC];
-    // every load unconditional (a clamped chunk index for the partial last chunk): the waitcnt
-    // pass then sees the same number of loads per tap and waits only for the set it stores,
-    // instead of vmcnt(0) behind a conditionally skipped load
-    auto wload = [&](int tap, u32x4 (&w)[NWC]) {
-      const u32x4* ws = reinterpret_cast<const u32x4*>(p.wT + (size_t)tap * COUT * COUT);
-#pragma unroll
-      for (int k = 0; k < NWC; ++k) {
-        const int i = ctid + 256 * k;
-        w[k] = ws[i < COUT * NC8 ? i : COUT * NC8 - 1];
-      }
-    };
-    auto wstore = [&](int slot, const u32x4 (&w)[NWC]) {
-      E* sw = sRing + slot * COUT * DCP;
-#pragma unroll
-      for (int k = 0; k < NWC; ++k) {
-        const int i = ctid + 256 * k;
-        if (k < COUT * NC8 / 256 || i < COUT * NC8) {
-          const int ci = i / NC8, k8 = i - ci * NC8;
-          *reinterpret_cast<u32x4*>(&sw[ci * DCP + k8 * 8]) = w[k];
-        }
-      }
-    };
-    wload(0, wr[0]);
-    wstore(0, wr[0]);
-#pragma unroll
-    for (int k = 1; k <= WPF; ++k) wload(k % 9, wr[k % WPF]);
-    if (ctid < 2) sCnt[ctid] = 0u;
-    unsigned gbt = 0u;
-    int qr[NPT], qc[NPT];
-    bool qv[NPT];
-#pragma unroll
-    for (int t = 0; t < NPT; ++t) {
-      const int q = (wave * NPT + t) * 32 + l32;
-      qv[t] = FULL || q < P;
-      qr[t] = qv[t] ? q / W : -1000;  // an invalid pixel never lands on the board
-      qc[t] = qv[t] ? q - qr[t] * W : -1000;
-    }
-    const int total = 9 * cnt;
-    for (int it = -1; it <= cnt; ++it) {
-      const bool conv = it >= 0 && it < cnt;
-      E* sD = sReg + (it & 1) * RE;
-      lds_barrier();  // A: dy(it) in its region, tap 0 in its slot
-      f32x16 acc[NPT][3];
-#pragma unroll
-      for (int t = 0; t < NPT; ++t)
-#pragma unroll
-        for (int ct = 0; ct < 3; ++ct)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) acc[t][ct][i] = 0.f;
-#pragma unroll 1
-      for (int t3 = 0; t3 < 9; t3 += WPF)
-#pragma unroll
-      for (int u = 0; u < WPF; ++u) {
-        const int tap = t3 + u;
-        if (tap) {  // T_tap
-          if (GB) grp_bar(&sCnt[0], gbt += 4u, lane);
-          else lds_barrier();
-        }
-        if (!conv) continue;
-        const int g = it * 9 + tap;
-        if (g + 1 < total) wstore((g + 1) & 1, wr[(u + 1) % WPF]);
-        wload((tap + 1 + WPF) % 9, wr[(u + 1) % WPF]);  // (past the last tap: unused, harmless)
-        const E* sW = sRing + (g & 1) * COUT * DCP;
-        const int dr = tap / 3 - 1, dc = tap % 3 - 1;
-        int aoff[NPT];
-#pragma unroll
-        for (int t = 0; t < NPT; ++t) {
-          const int sr = qr[t] - dr, sc = qc[t] - dc;
-          const bool v = (unsigned)sr < (unsigned)H && (unsigned)sc < (unsigned)W;
-          aoff[t] = (v ? sr * W + sc : P) * DCP + 8 * hh;
-        }
-        E8 A[2][3], B[2][NPT];  // A: W^T (32 ci x 16 co), B: dy (16 co x 32 px)
-        auto ld = [&](int ks, E8 (&a)[3], E8 (&b)[NPT]) {
-#pragma unroll
-          for (int ct = 0; ct < 3; ++ct)
-            a[ct] = *reinterpret_cast<const E8*>(&sW[(ct * 32 + l32) * DCP + ks * 16 + 8 * hh]);
-#pragma unroll
-          for (int t = 0; t < NPT; ++t) b[t] = *reinterpret_cast<const E8*>(&sD[aoff[t] + ks * 16]);
-        };
-        ld(0, A[0], B[0]);
-        __builtin_amdgcn_sched_group_barrier(0x100, NPT + 3, 0);
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          if (ks + 1 < KS) {
-            ld(ks + 1, A[(ks + 1) & 1], B[(ks + 1) & 1]);
-            __builtin_amdgcn_sched_group_barrier(0x100, NPT + 3, 0);
-          }
-#pragma unroll
-          for (int t = 0; t < NPT; ++t)
-#pragma unroll
-            for (int ct = 0; ct < 3; ++ct) acc[t][ct] = mfma32(A[ks & 1][ct], B[ks & 1][t], acc[t][ct]);
-          __builtin_amdgcn_sched_group_barrier(0x008, 3 * NPT, 0);
-        }
-      }
-      if (GB) grp_bar(&sCnt[0], gbt += 4u, lane);  // X1: every dgrad wave's reads of dy(it) done
-      else lds_barrier();
-      if (conv) {
-#pragma unroll
-        for (int t = 0; t < NPT; ++t) {
-          const int px = (wave * NPT + t) * 32 + l32;
-          if (qv[t]) {
-#pragma unroll
-            for (int ct = 0; ct < 3; ++ct)
-#pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                E4 q4;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) q4[e] = (E)acc[t][ct][4 * j + e];
-                *reinterpret_cast<E4*>(&sD[px * DCP + ct * 32 + 8 * j + 4 * hh]) = q4;
-              }
-          }
-        }
-      }
-    }
-  } else {
-    // =============================== memory waves ===============================
-    const int mtid = threadIdx.x - 256;
-    const float inv_cnt = 1.0f / (16.0f * (float)P);
-    unsigned gbt = 0u;
-#define MEM_BAR()                                  \
-  do {                                             \
-    if (GB) grp_bar(&sCnt[1], gbt += 4u, lane);    \
-    else lds_barrier();                            \
-  } while (0)
-    float gam = 0.f, acc_g = 0.f, acc_b = 0.f, acc_bias = 0.f;  // mtid < 96: channel mtid
-    if (mtid < COUT) gam = p.gamma[mtid];
-    if (mtid < DCP / 8) {
-      *reinterpret_cast<u32x4*>(&sReg[P * DCP + 8 * mtid]) = u32x4{0u, 0u, 0u, 0u};
-      *reinterpret_cast<u32x4*>(&sReg[RE + P * DCP + 8 * mtid]) = u32x4{0u, 0u, 0u, 0u};
-    }
-    u32x4 ad[NCH];  // the only registers carried across iterations
-    // (declared per iteration, so that nothing but ad is live across the loop's back edge)
-#define WSB_GLOAD_VARS                           \
-  u32x4 dv[NCH], yr[NCH];                        \
-  uint32_t mv[NCH];                              \
-  float dm[8], smean = 0.f, srstd = 0.f, cmean = 0.f, crstd = 0.f
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) ad[i] = u32x4{0u, 0u, 0u, 0u};
-    for (int it = -1; it <= cnt; ++it) {
-      const int e = it - 1, f = it + 1;
-      const int rg = (it + 1) & 1;  // region of samples e and f
-      E* sD = sReg + rg * RE;
-      const size_t ne = (size_t)blockIdx.x + (size_t)e * G, nf = (size_t)blockIdx.x + (size_t)f * G;
-      const bool pf = f < cnt;
-      WSB_GLOAD_VARS;
-      float s1[8], s2[8], s3[8], S1 = 0.f, S3 = 0.f;
-      // loop-variant thread coordinates: the per-chunk address math stays inside the loop
-      // (hoisted out of it, the 13 chunks' 64-bit addresses of each stream would be spilled)
-      const int mtid = threadIdx.x - 256 + opaque0();
-      const int pg = mtid / NC8, c8 = mtid - pg * NC8, grp = c8 >> 1;
-      const bool gact = mtid < PG * NC8;
-      auto gload = [&](int n, u32x4 (&dv)[NCH], u32x4 (&yr)[NCH], uint32_t (&mv)[NCH], float (&dm)[8], float& smean,
-                       float& srstd, float& cmean, float& crstd) {  // pass-1 inputs of sample n
-  #pragma unroll
-        for (int i = 0; i < NCH; ++i) {
-          const int px = pg + PG * i;
-          dv[i] = yr[i] = u32x4{0u, 0u, 0u, 0u};
-          mv[i] = 0u;
-          if (gact && px < P) {
-            const size_t o = ((size_t)n * P + px) * COUT + c8 * 8;
-            dv[i] = *reinterpret_cast<const u32x4*>(&p.dout[o]);
-            mv[i] = p.rmask[((size_t)n * P + px) * NC8 + c8];
-            yr[i] = *reinterpret_cast<const u32x4*>(&p.y[o]);
-          }
-        }
-  #pragma unroll
-        for (int j = 0; j < 8; ++j) dm[j] = 1.f;
-        if (gact) {
-          if (p.dmask) {
-  #pragma unroll
-            for (int j = 0; j < 8; ++j) dm[j] = p.dmask[(size_t)n * COUT + c8 * 8 + j];
-          }
-          smean = p.stats[((size_t)n * NGRP + grp) * 2];
-          srstd = p.stats[((size_t)n * NGRP + grp) * 2 + 1];
-        }
-        if (mtid < COUT) {
-          cmean = p.stats[((size_t)n * NGRP + (mtid >> 4)) * 2];
-          crstd = p.stats[((size_t)n * NGRP + (mtid >> 4)) * 2 + 1];
-        }
-      };
-      auto aload = [&](int n) {  // the skip-gradient addend of sample n (its dx leaves next iteration)
-  #pragma unroll
-        for (int i = 0; i < NCH; ++i) {
-          const int px = pg + PG * i;
-          ad[i] = u32x4{0u, 0u, 0u, 0u};
-          if (p.addend && gact && px < P)
-            ad[i] = *reinterpret_cast<const u32x4*>(&p.addend[((size_t)n * P + px) * COUT + c8 * 8]);
-        }
-      };
-      lds_barrier();  // A
-      if (e >= 0 && gact) {  // ---- dx(e) (+ addend) from its staging image ----
-#pragma unroll
-        for (int i = 0; i < NCH; ++i) {
-          const int px = pg + PG * i;
-          if (px < P) {
-            const E8 a8 = __builtin_bit_cast(E8, *reinterpret_cast<const u32x4*>(&sD[px * DCP + c8 * 8]));
-            const E8 r8 = __builtin_bit_cast(E8, ad[i]);
-            E8 s8;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) s8[j] = (E)((float)a8[j] + (float)r8[j]);
-            *reinterpret_cast<u32x4*>(&p.dx[(ne * P + px) * COUT + c8 * 8]) = __builtin_bit_cast(u32x4, s8);
-          }
-        }
-      }
-      // sample f's pass-1 inputs, issued once the addend registers are free
-      asm volatile("" ::: "memory");
-      if (pf) gload((int)nf, dv, yr, mv, dm, smean, srstd, cmean, crstd);
-      MEM_BAR();  // T1: dx(e) read; the region takes dz(f)
-      if (!GB) lds_barrier();  // T2
-      if (pf && gact) {  // ---- pass 1: dz and the channel sums ----
-#pragma unroll
-        for (int j = 0; j < 8; ++j) s1[j] = s2[j] = s3[j] = 0.f;
-#pragma unroll
-        for (int i = 0; i < NCH; ++i) {
-          const int px = pg + PG * i;
-          if (px < P) {
-            const E8 d8 = __builtin_bit_cast(E8, dv[i]);
-            const E8 y8 = __builtin_bit_cast(E8, yr[i]);
-            E8 z8;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const float d = (float)d8[j] * dm[j];
-              z8[j] = (E)(((mv[i] >> j) & 1u) ? d : 0.f);
-              const float zf = (float)z8[j];
-              const float yh = ((float)y8[j] - smean) * srstd;
-              s1[j] += zf;
-              s2[j] += zf * yh;
-              s3[j] += yh;
-            }
-            *reinterpret_cast<u32x4*>(&sD[px * DCP + c8 * 8]) = __builtin_bit_cast(u32x4, z8);
-          }
-        }
-        if (pg < WSB_FOLD) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            sRed[(pg * 3 + 0) * COUT + c8 * 8 + j] = s1[j];
-            sRed[(pg * 3 + 1) * COUT + c8 * 8 + j] = s2[j];
-            sRed[(pg * 3 + 2) * COUT + c8 * 8 + j] = s3[j];
-          }
-        }
-      }
-      // dout consumed: its registers take the addend (the clobber keeps the scheduler from hoisting
-      // these loads above pass 1, where dout, y and the addend would all be live)
-      asm volatile("" ::: "memory");
-      if (it >= 0 && it < cnt) aload((int)blockIdx.x + it * G);
-      MEM_BAR();  // T3
-      if (pf && gact && pg >= WSB_FOLD) {
-        const int q = pg - WSB_FOLD;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          sRed[(q * 3 + 0) * COUT + c8 * 8 + j] += s1[j];
-          sRed[(q * 3 + 1) * COUT + c8 * 8 + j] += s2[j];
-          sRed[(q * 3 + 2) * COUT + c8 * 8 + j] += s3[j];
-        }
-      }
-      MEM_BAR();  // T4
-      if (pf && mtid < COUT) {
-        float S2 = 0.f;
-        S1 = S3 = 0.f;
-        for (int q = 0; q < WSB_FOLD; ++q) {
-          S1 += sRed[(q * 3 + 0) * COUT + mtid];
-          S2 += sRed[(q * 3 + 1) * COUT + mtid];
-          S3 += sRed[(q * 3 + 2) * COUT + mtid];
-        }
-        sTmp[mtid] = gam * S1;
-        sTmp[COUT + mtid] = gam * S2;
-        acc_g += S2;
-        acc_b += S1;
-      }
-      MEM_BAR();  // T5
-      if (pf && mtid < COUT) {
-        const int g0 = (mtid >> 4) * 16;
-        float m1 = 0.f, m2 = 0.f;
-        for (int k = 0; k < 16; ++k) {
-          m1 += sTmp[g0 + k];
-          m2 += sTmp[COUT + g0 + k];
-        }
-        m1 *= inv_cnt;
-        m2 *= inv_cnt;
-        sCo[mtid] = crstd * gam;
-        sCo[COUT + mtid] = -crstd * crstd * m2;
-        sCo[2 * COUT + mtid] = crstd * (crstd * m2 * cmean - m1);
-        acc_bias += crstd * (gam * S1 - (float)P * m1 - m2 * S3);
-      }
-      MEM_BAR();  // T6
-      if (pf && gact) {  // ---- pass 2: dy (GroupNorm backward) -> LDS + HBM ----
-        float A[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) A[j] = sCo[c8 * 8 + j];
-        const float Bg = sCo[COUT + c8 * 8], Cg = sCo[2 * COUT + c8 * 8];
-#pragma unroll
-        for (int i = 0; i < NCH; ++i) {
-          const int px = pg + PG * i;
-          if (px < P) {
-            const size_t o = (nf * P + px) * COUT + c8 * 8;
-            const u32x4 zv = *reinterpret_cast<const u32x4*>(&sD[px * DCP + c8 * 8]);
-            if (p.dz) *reinterpret_cast<u32x4*>(&p.dz[o]) = zv;
-            const E8 z8 = __builtin_bit_cast(E8, zv);
-            const E8 y8 = __builtin_bit_cast(E8, yr[i]);
-            E8 d8;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) d8[j] = (E)(A[j] * (float)z8[j] + Bg * (float)y8[j] + Cg);
-            const u32x4 v = __builtin_bit_cast(u32x4, d8);
-            *reinterpret_cast<u32x4*>(&sD[px * DCP + c8 * 8]) = v;
-            *reinterpret_cast<u32x4*>(&p.dy[o]) = v;
-          }
-        }
-      }
-      if (!GB) {
-        lds_barrier();  // T7
-        lds_barrier();  // T8
-        lds_barrier();  // X1
-      }
-    }
-#undef WSB_GLOAD_VARS
-#undef MEM_BAR
-    if (mtid < COUT) {
-      p.part[((size_t)blockIdx.x * 3 + 0) * COUT + mtid] = acc_g;
-      p.part[((size_t)blockIdx.x * 3 + 1) * COUT + mtid] = acc_b;
-      p.part[((size_t)blockIdx.x * 3 + 2) * COUT + mtid] = acc_bias;
-    }
   }
 }
 
@@ -1198,33 +826,10 @@ void launch_bwd_data(const BwdDataParams<E>& p, int grid, size_t lds, hipStream_
   else launch_bwd_data_t<E, NPT, DGRAD, NCH, false>(p, grid, lds, s);
 }
 
-template <typename E, int NPT, bool FULL, bool GB>
-void launch_bwd_data_ws_t(const BwdDataParams<E>& p, int grid, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    set_lds_attr(k_bwd_data_ws<E, NPT, FULL, GB>);
-    attr = true;
-  }
-  hipLaunchKernelGGL((k_bwd_data_ws<E, NPT, FULL, GB>), dim3(grid), dim3(512), wsb_lds_bytes(p.H * p.W), s, p);
-}
-template <typename E, int NPT, bool FULL>
-void launch_bwd_data_ws(const BwdDataParams<E>& p, int grid, hipStream_t s) {
-  if (g_variant[MCV_BWD] == 3) launch_bwd_data_ws_t<E, NPT, FULL, true>(p, grid, s);
-  else launch_bwd_data_ws_t<E, NPT, FULL, false>(p, grid, s);
-}
-
 // grid: in, the per-sample kernel's grid; out, the workgroups launched (= partial rows in p.part)
 template <typename E, bool DGRAD>
 int dispatch_bwd_data(const BwdDataParams<E>& p, int& grid, hipStream_t s) {
   const int P = p.H * p.W;
-  if (DGRAD && P <= 256 && p.rmask && g_variant[MCV_BWD] >= 2) {  // opt-in until measured faster
-    const int ncu = num_cus();
-    grid = p.N < ncu ? p.N : ncu;
-    if (P == 256) launch_bwd_data_ws<E, 2, true>(p, grid, s);
-    else if (P > 128) launch_bwd_data_ws<E, 2, false>(p, grid, s);
-    else launch_bwd_data_ws<E, 1, false>(p, grid, s);
-    return MS_OK;
-  }
   const size_t lds = (size_t)bwd_data_lds(P);
   if (lds > 160 * 1024) {
     snprintf(g_err, sizeof g_err, "mc_conv_gn_bwd: board %dx%d needs %zu B LDS", p.H, p.W, lds);
@@ -1273,6 +878,39 @@ int check_launch(const char* what) {
 }
 
 template <typename E>
+int run_wgrad(const Plan& pl, const uint16_t* dy, const uint16_t* x, float* dw, float* work, int32_t n, int32_t h,
+              int32_t w_, int32_t cin, hipStream_t s) {
+  WgradParams<E> wp;
+  wp.dy = reinterpret_cast<const E*>(dy);
+  wp.x = reinterpret_cast<const E*>(x);
+  wp.part = work + pl.gn_part;
+  wp.N = n;
+  wp.H = h;
+  wp.W = w_;
+  wp.G = pl.G;
+#ifdef MC_WSX
+  wp.exp = g_wgrad_exp;
+#else
+  wp.exp = 0;
+#endif
+  const size_t lds = (size_t)wgrad_lds(h, w_);
+  if (pl.c96) {
+    static bool attr = false;
+    if (!attr) {
+      set_lds_attr(k_wgrad_c96<E>);
+      attr = true;
+    }
+    hipLaunchKernelGGL(k_wgrad_c96<E>, dim3(pl.grid_w), dim3(512), (size_t)WC_LDS, s, wp);
+  } else if (cin == 96) launch_wgrad<E, 96>(wp, pl.grid_w, lds, s);
+  else launch_wgrad<E, 16>(wp, pl.grid_w, lds, s);
+  int rc;
+  if ((rc = check_launch("k_wgrad"))) return rc;
+  const int64_t nw = (int64_t)9 * COUT * cin;
+  launch_reduce((const float*)(work + pl.gn_part), pl.G, nw, dw, s);
+  return check_launch("k_reduce");
+}
+
+template <typename E>
 int run_bwd(const uint16_t* dout, const uint16_t* out, const uint8_t* relu_mask, const uint16_t* ysave,
             const float* stats, const float* gamma, const float* dmask, const uint16_t* x, const uint16_t* wT,
             const uint16_t* addend, uint16_t* dy, uint16_t* dz, uint16_t* dx, float* dw, float* dgn, float* work,
@@ -1301,34 +939,7 @@ int run_bwd(const uint16_t* dout, const uint16_t* out, const uint8_t* relu_mask,
   if ((rc = check_launch("k_bwd_data"))) return rc;
   launch_reduce((const float*)work, grid_d, (int64_t)3 * COUT, dgn, s);
   if ((rc = check_launch("k_reduce"))) return rc;
-
-  WgradParams<E> wp;
-  wp.dy = reinterpret_cast<const E*>(dy);
-  wp.x = reinterpret_cast<const E*>(x);
-  wp.part = work + pl.gn_part;
-  wp.N = n;
-  wp.H = h;
-  wp.W = w_;
-  wp.G = pl.G;
-#ifdef MC_WSX
-  wp.exp = g_wgrad_exp;
-#else
-  wp.exp = 0;
-#endif
-  const size_t lds = (size_t)wgrad_lds(h, w_);
-  if (pl.c96) {
-    static bool attr = false;
-    if (!attr) {
-      set_lds_attr(k_wgrad_c96<E>);
-      attr = true;
-    }
-    hipLaunchKernelGGL(k_wgrad_c96<E>, dim3(pl.grid_w), dim3(512), (size_t)WC_LDS, s, wp);
-  } else if (cin == 96) launch_wgrad<E, 96>(wp, pl.grid_w, lds, s);
-  else launch_wgrad<E, 16>(wp, pl.grid_w, lds, s);
-  if ((rc = check_launch("k_wgrad"))) return rc;
-  const int64_t nw = (int64_t)9 * COUT * cin;
-  launch_reduce((const float*)(work + pl.gn_part), pl.G, nw, dw, s);
-  return check_launch("k_reduce");
+  return run_wgrad<E>(pl, dy, x, dw, work, n, h, w_, cin, s);
 }
 
 }  // namespace
@@ -1344,6 +955,29 @@ int64_t mc_conv_gn_bwd_workspace(int32_t n, int32_t h, int32_t w_, int32_t cin) 
   if (n <= 0 || h <= 0 || w_ <= 0 || (cin != 16 && cin != 96)) return -1;
   const Plan pl = make_plan(n, h, w_, cin);
   return pl.gn_part + pl.w_part;
+}
+
+int mc_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* work, int64_t work_floats, int32_t n,
+                  int32_t h, int32_t w_, int32_t cin, int32_t dtype, void* stream) {
+  if (!dy || !x || !dw || !work || n <= 0 || h <= 0 || w_ <= 0 || (cin != 16 && cin != 96)) {
+    snprintf(g_err, sizeof g_err, "mc_conv_wgrad: bad argument");
+    return MS_EINVAL;
+  }
+  const Plan pl = make_plan(n, h, w_, cin);
+  if (work_floats < pl.gn_part + pl.w_part) {
+    snprintf(g_err, sizeof g_err, "mc_conv_wgrad: workspace %lld < %lld floats", (long long)work_floats,
+             (long long)(pl.gn_part + pl.w_part));
+    return MS_EINVAL;
+  }
+  if (wgrad_lds(h, w_) > 160 * 1024) {
+    snprintf(g_err, sizeof g_err, "mc_conv_wgrad: board %dx%d too large", h, w_);
+    return MS_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MC_DT_BF16) return run_wgrad<__bf16>(pl, dy, x, dw, work, n, h, w_, cin, s);
+  if (dtype == MC_DT_F16) return run_wgrad<_Float16>(pl, dy, x, dw, work, n, h, w_, cin, s);
+  snprintf(g_err, sizeof g_err, "mc_conv_wgrad: dtype %d unsupported (0 bf16, 1 f16)", dtype);
+  return MS_EINVAL;
 }
 
 int mc_conv_gn_bwd(const uint16_t* dout, const uint16_t* out, const uint8_t* relu_mask, const uint16_t* ysave,

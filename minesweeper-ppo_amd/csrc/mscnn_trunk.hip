@@ -1,0 +1,933 @@
+// mscnn_trunk.hip — the whole residual stack in one launch per direction (gfx950 MFMA).
+//
+// Reference chain (minesweeper/models/cnn_residual.py:7-27, 55-56): `blocks` x
+//   a1  = Dropout2d(ReLU(GN1(conv1(x))))
+//   out = ReLU(GN2(conv2(a1)) + x)
+// mscnn.hip / mscnn_bwd.hip run one launch per conv layer: every layer reads its input and
+// residual from HBM and writes its output back, and every layer backward reads dout and writes
+// dx, so the activations make one HBM round trip per layer and direction. Here one persistent
+// workgroup (4 waves) carries a sample through ALL the layers, and a layer's output goes
+// straight into the LDS tile the next layer's implicit GEMM reads:
+//
+//   k_trunk_fwd  per sample: stage block 0's input once; per layer: 9-tap implicit GEMM on
+//                v_mfma_f32_32x32x16 (the per-layer kernel's tap loop), GroupNorm statistics,
+//                y -> LDS, epilogue (affine, residual, ReLU, dropout) written IN PLACE over the
+//                input tile (the layouts coincide: [P+1][104] padded rows), stored to HBM only
+//                where the backward or the caller needs it (y, out, ReLU bits, statistics).
+//                The block input needed by conv2's residual is re-read from the block output
+//                the workgroup wrote two layers earlier (L2 / Infinity Cache); without saved
+//                outputs (no-grad forward) it goes to a per-workgroup slot of the workspace.
+//   k_trunk_bwd  per sample, layers in reverse: GroupNorm backward (pass 1: dz and channel
+//                sums; pass 2: dy to LDS and to HBM for the weight gradient), then the data
+//                gradient dx = sum_tap shift(dy) . W^T on the MFMA, staged in LDS where the
+//                NEXT layer's pass 1 reads it as its dout. The skip gradient of a block (dz of
+//                its conv2) waits in a per-workgroup slot of the workspace for two layers and
+//                is added where the block input's gradient is formed. The stem's GroupNorm
+//                backward closes the chain (its input needs no gradient). d gamma / d beta /
+//                d bias per layer accumulate per workgroup (fixed sample order) and are summed
+//                over workgroups by k_reduce: deterministic.
+//
+// Every arithmetic step is the per-layer kernels' (same accumulation order, same roundings to
+// the 16-bit type at the same points), so the outputs are bitwise those of the per-layer path
+// (tests/test_trunk_gpu.py). The weight gradients stay per-layer launches (mc_conv_wgrad).
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/msenv.h"
+#include "../../include/mscnn.h"
+#include "mscnn_common.h"
+
+namespace {
+
+using namespace mc;
+
+constexpr int CINP = COUT + 8;  // padded pixel row (elements): conflict-free ds_read_b128 row reads
+constexpr int C8 = COUT / 8;    // 16-B chunks per pixel row
+constexpr int MAXL = MC_TRUNK_MAX_LAYERS;
+
+template <typename E>
+struct TFLayer {
+  const E* wt;          // [9][96][96] (tap, co, ci)
+  const float* bias;    // [96]
+  const float* gamma;   // [96]
+  const float* beta;    // [96]
+  const float* dmask;   // [N][96] Dropout2d scale (0 or 1/(1-p)) after the ReLU, or NULL
+  E* out;               // [N][P][96] or NULL
+  E* ysave;             // [N][P][96] or NULL
+  float* stats;         // [N][6][2] (mean, rstd) or NULL
+  uint8_t* rmask;       // [N][P][12] ReLU bits or NULL
+};
+
+template <typename E>
+struct TrunkFwdParams {
+  const E* x0;  // [N][P][96] block 0's input
+  E* ws;        // [grid][P][96]: block outputs that are not kept (residual of the next block)
+  int NL, N, H, W;
+  float eps;
+  TFLayer<E> L[MAXL];
+};
+
+__host__ __device__ inline int tf_region(int P) { return ((P + 1) * CINP + 7) & ~7; }
+__host__ __device__ inline size_t tf_lds(int P) {
+  return (size_t)tf_region(P) * 2 + (size_t)COUT * CINP * 2 + WAVES * NGRP * 4 + 3 * COUT * 4;
+}
+
+// 16-B chunk k of this thread's share of a [P][96] tile: c = tid + 256k, pixel c / 12, chunk c % 12
+template <typename E, int NWC>
+__device__ __forceinline__ void load_wtap(const E* wt, int tap, int tid, u32x4 (&v)[NWC]) {
+  const u32x4* ws = reinterpret_cast<const u32x4*>(wt + (size_t)tap * COUT * COUT);
+#pragma unroll
+  for (int k = 0; k < NWC; ++k) {
+    const int i = tid + 256 * k;
+    if (k < COUT * C8 / 256 || i < COUT * C8) v[k] = ws[i];  // the first 4 chunks are always full
+  }
+}
+template <typename E, int NWC>
+__device__ __forceinline__ void store_wtap(E* sW, int tid, const u32x4 (&v)[NWC]) {
+#pragma unroll
+  for (int k = 0; k < NWC; ++k) {
+    const int i = tid + 256 * k;
+    if (k < COUT * C8 / 256 || i < COUT * C8) {
+      const int r = i / C8, c = i - r * C8;
+      *reinterpret_cast<u32x4*>(&sW[r * CINP + c * 8]) = v[k];
+    }
+  }
+}
+
+// LDS: sX [P+1][104] (row P zero): the layer's input tile; after its conv the same bytes hold y,
+// then the layer's output (the next layer's input). sW [96][104]: one weight tap.
+// f32 sRed [4][6] (statistics exchange), sAB [3][96] (scale, shift, dropout scale).
+template <typename E, int NPT, bool FULL>
+__global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_fwd(TrunkFwdParams<E> p) {
+  // no contraction: every expression rounds the same way in the per-layer and the one-launch
+  // kernels (explicit fmaf where a fused multiply-add is wanted), so they agree bitwise
+#pragma clang fp contract(off)
+  typedef typename EV<E>::v8 E8;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NEC = (NPT * 128 * C8 + 255) / 256;  // 16-B chunks of a sample tile per thread
+  constexpr int NWC = (COUT * C8 + 255) / 256;       // 16-B chunks of a weight tap per thread
+  const int H = p.H, W = p.W, P = H * W;
+  E* sX = reinterpret_cast<E*>(smem);
+  E* sW = sX + tf_region(P);
+  float* sRed = reinterpret_cast<float*>(sW + COUT * CINP);
+  float* sAB = sRed + WAVES * NGRP;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const float inv_cnt = 1.0f / (16.0f * (float)P);
+
+  int qr[NPT], qc[NPT];  // this lane's output pixel of each 32-pixel tile
+#pragma unroll
+  for (int t = 0; t < NPT; ++t) {
+    const int q = (wave * NPT + t) * 32 + l32;
+    qr[t] = q < P ? q / W : -1000;  // a pixel past P reads the zero row at every tap
+    qc[t] = q < P ? q - qr[t] * W : -1000;
+  }
+  u32x4 wr[NWC];
+
+  for (int n = blockIdx.x; n < p.N; n += gridDim.x) {
+    const size_t so = (size_t)n * P * COUT;  // this sample's offset in every [N][P][96] tensor
+    {  // stage block 0's input and layer 0's tap-0 weights
+      const int tid = threadIdx.x + opaque0();
+      u32x4 xin[NEC];
+      const u32x4* xs = reinterpret_cast<const u32x4*>(p.x0 + so);
+#pragma unroll
+      for (int k = 0; k < NEC; ++k) {
+        const int i = tid + 256 * k;
+        if (FULL || i < P * C8) xin[k] = xs[i];
+      }
+      load_wtap<E, NWC>(p.L[0].wt, 0, tid, wr);
+      for (int i = tid; i < C8; i += 256) *reinterpret_cast<u32x4*>(&sX[P * CINP + i * 8]) = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int k = 0; k < NEC; ++k) {
+        const int i = tid + 256 * k;
+        if (FULL || i < P * C8) {
+          const int px = i / C8, c8 = i - px * C8;
+          *reinterpret_cast<u32x4*>(&sX[px * CINP + c8 * 8]) = xin[k];
+        }
+      }
+      store_wtap<E, NWC>(sW, tid, wr);
+    }
+    __syncthreads();
+
+    for (int l = 0; l < p.NL; ++l) {
+      // loop-variant thread coordinates: the per-chunk address math and the taps' row offsets
+      // are recomputed per layer instead of hoisted out of this loop (they would be spilled)
+      const int tid = threadIdx.x + opaque0();
+#pragma unroll
+      for (int t = 0; t < NPT; ++t) asm volatile("" : "+v"(qr[t]), "+v"(qc[t]));
+      const E* wt = p.L[l].wt;
+      float biasv[3];
+#pragma unroll
+      for (int ct = 0; ct < 3; ++ct) biasv[ct] = p.L[l].bias[ct * 32 + l32];
+
+      f32x16 acc[NPT][3];
+#pragma unroll
+      for (int t = 0; t < NPT; ++t)
+#pragma unroll
+        for (int ct = 0; ct < 3; ++ct)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) acc[t][ct][i] = 0.f;
+
+      for (int tap = 0; tap < 9; ++tap) {
+        if (tap + 1 < 9) load_wtap<E, NWC>(wt, tap + 1, tid, wr);
+        const int dr = tap / 3 - 1, dc = tap % 3 - 1;
+        int aoff[NPT];
+#pragma unroll
+        for (int t = 0; t < NPT; ++t) {
+          const int sr = qr[t] + dr, sc = qc[t] + dc;
+          const bool v = (unsigned)sr < (unsigned)H && (unsigned)sc < (unsigned)W;
+          aoff[t] = (v ? sr * W + sc : P) * CINP + 8 * hh;
+        }
+        // 6 k steps, operands double-buffered, order pinned: step k+1's LDS reads before step k's MFMAs
+        constexpr int KS = COUT / 16;
+        E8 A[2][NPT], B[2][3];
+        auto ld = [&](int ks, E8 (&a)[NPT], E8 (&b)[3]) {
+#pragma unroll
+          for (int ct = 0; ct < 3; ++ct)
+            b[ct] = *reinterpret_cast<const E8*>(&sW[(ct * 32 + l32) * CINP + ks * 16 + 8 * hh]);
+#pragma unroll
+          for (int t = 0; t < NPT; ++t) a[t] = *reinterpret_cast<const E8*>(&sX[aoff[t] + ks * 16]);
+        };
+        ld(0, A[0], B[0]);
+        __builtin_amdgcn_sched_group_barrier(0x100, NPT + 3, 0);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          if (ks + 1 < KS) {
+            ld(ks + 1, A[(ks + 1) & 1], B[(ks + 1) & 1]);
+            __builtin_amdgcn_sched_group_barrier(0x100, NPT + 3, 0);
+          }
+#pragma unroll
+          for (int t = 0; t < NPT; ++t)
+#pragma unroll
+            for (int ct = 0; ct < 3; ++ct) acc[t][ct] = mfma32(A[ks & 1][t], B[ks & 1][ct], acc[t][ct]);
+          __builtin_amdgcn_sched_group_barrier(0x008, 3 * NPT, 0);
+        }
+        __syncthreads();  // sW (and after the last tap sX) fully read
+        if (tap + 1 < 9) {
+          store_wtap<E, NWC>(sW, tid, wr);
+          __syncthreads();
+        }
+      }
+      // the next layer's tap-0 weights: loaded now, written to sW (free) after the statistics
+      const bool more = l + 1 < p.NL;
+      if (more) load_wtap<E, NWC>(p.L[l + 1].wt, 0, tid, wr);
+
+      // ---------------- GroupNorm statistics (two-pass, as the per-layer kernel) ----------------
+      float gmean[NGRP], grstd[NGRP];
+      for (int pass = 0; pass < 2; ++pass) {
+        float part[3];
+#pragma unroll
+        for (int ct = 0; ct < 3; ++ct) {
+          const float mu = pass ? gmean[2 * ct + (l32 >> 4)] : 0.f;
+          float v[NPT * 16];
+#pragma unroll
+          for (int t = 0; t < NPT; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const int px = (wave * NPT + t) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+              const float d = acc[t][ct][i] + biasv[ct] - mu;
+              v[t * 16 + i] = (FULL || px < P) ? (pass ? d * d : d) : 0.f;
+            }
+#pragma unroll
+          for (int w2 = NPT * 8; w2 >= 1; w2 >>= 1)
+#pragma unroll
+            for (int i = 0; i < w2; ++i) v[i] += v[i + w2];
+          part[ct] = row_sum16(v[0]);
+        }
+        float gs[3][2];
+#pragma unroll
+        for (int ct = 0; ct < 3; ++ct) {
+          gs[ct][0] = readlane_f(part[ct], 15) + readlane_f(part[ct], 47);
+          gs[ct][1] = readlane_f(part[ct], 31) + readlane_f(part[ct], 63);
+        }
+        if (lane == 0) {
+#pragma unroll
+          for (int ct = 0; ct < 3; ++ct) {
+            sRed[wave * NGRP + 2 * ct] = gs[ct][0];
+            sRed[wave * NGRP + 2 * ct + 1] = gs[ct][1];
+          }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int g = 0; g < NGRP; ++g) {
+          float tot = 0.f;
+#pragma unroll
+          for (int w = 0; w < WAVES; ++w) tot += sRed[w * NGRP + g];
+          if (pass == 0) gmean[g] = tot * inv_cnt;
+          else grstd[g] = rsqrtf(tot * inv_cnt + p.eps);
+        }
+        __syncthreads();  // sRed reused by the next pass
+      }
+      float* stats = p.L[l].stats;
+      if (stats && tid < NGRP) {
+        float m = 0.f, r = 0.f;
+#pragma unroll
+        for (int g = 0; g < NGRP; ++g)
+          if (g == tid) {
+            m = gmean[g];
+            r = grstd[g];
+          }
+        stats[((size_t)n * NGRP + tid) * 2 + 0] = m;
+        stats[((size_t)n * NGRP + tid) * 2 + 1] = r;
+      }
+      // y -> LDS over the (fully read) input tile, in the tile's padded layout
+#pragma unroll
+      for (int ct = 0; ct < 3; ++ct)
+#pragma unroll
+        for (int t = 0; t < NPT; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int px = (wave * NPT + t) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+            if (FULL || px < P) sX[px * CINP + ct * 32 + l32] = (E)(acc[t][ct][i] + biasv[ct]);
+          }
+      if (more) store_wtap<E, NWC>(sW, tid, wr);
+      if (tid < COUT) {  // z = y * scale + shift (+ res), then ReLU, then * dropout scale
+        const int g = tid >> 4;
+        float mu = 0.f, rs = 0.f;
+#pragma unroll
+        for (int gg = 0; gg < NGRP; ++gg)
+          if (gg == g) {
+            mu = gmean[gg];
+            rs = grstd[gg];
+          }
+        const float a = p.L[l].gamma[tid] * rs;
+        sAB[tid] = a;
+        sAB[COUT + tid] = p.L[l].beta[tid] - mu * a;
+        const float* dmask = p.L[l].dmask;
+        sAB[2 * COUT + tid] = dmask ? dmask[(size_t)n * COUT + tid] : 1.0f;
+      }
+      __syncthreads();
+
+      // ---------------- epilogue: 16-B chunks of [px][co], written in place ----------------
+      // residual (conv2 of block b): the block input = block 0's input, or block b-1's output
+      const E* res = nullptr;
+      if (l & 1) {
+        if (l == 1) res = p.x0 + so;
+        else res = p.L[l - 2].out ? p.L[l - 2].out + so : p.ws + (size_t)blockIdx.x * P * COUT;
+      }
+      E* out = p.L[l].out ? p.L[l].out + so : nullptr;
+      if (!out && (l & 1) && more) out = p.ws + (size_t)blockIdx.x * P * COUT;  // the next block's residual
+      E* ysave = p.L[l].ysave ? p.L[l].ysave + so : nullptr;
+      uint8_t* rmask = p.L[l].rmask ? p.L[l].rmask + (size_t)n * P * C8 : nullptr;
+      float ca[3][8], cb[3][8], cd[3][8];
+#pragma unroll
+      for (int j3 = 0; j3 < 3; ++j3) {
+        const int cg = ((tid % C8) + 4 * j3) % C8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          ca[j3][j] = sAB[cg * 8 + j];
+          cb[j3][j] = sAB[COUT + cg * 8 + j];
+          cd[j3][j] = sAB[2 * COUT + cg * 8 + j];
+        }
+      }
+      // residual chunks are loaded RB at a time, all of a batch before its first store (a load
+      // issued after a store waits for that store too: vmcnt counts both)
+      constexpr int RB = (NEC + 1) / 2;
+      u32x4 rq[RB];
+#pragma unroll
+      for (int k = 0; k < NEC; ++k) {
+        const int c = tid + 256 * k;
+        if (k % RB == 0) {
+#pragma unroll
+          for (int u = 0; u < RB; ++u) {
+            const int cu = tid + 256 * (k + u);
+            rq[u] = u32x4{0u, 0u, 0u, 0u};
+            if (res && k + u < NEC && (FULL || cu < P * C8)) rq[u] = *reinterpret_cast<const u32x4*>(&res[(size_t)cu * 8]);
+          }
+        }
+        if (FULL || c < P * C8) {
+          const int px = c / C8, c8 = c - px * C8;
+          E* sp = &sX[px * CINP + c8 * 8];
+          const u32x4 yv = *reinterpret_cast<const u32x4*>(sp);
+          if (ysave) *reinterpret_cast<u32x4*>(&ysave[(size_t)c * 8]) = yv;
+          const E8 y8 = __builtin_bit_cast(E8, yv);
+          const E8 r8 = __builtin_bit_cast(E8, rq[k % RB]);
+          E8 o8;
+          uint32_t mb = 0u;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float z = fmaxf(__builtin_fmaf((float)y8[j], ca[k % 3][j], cb[k % 3][j]) + (float)r8[j], 0.f);
+            o8[j] = (E)(z * cd[k % 3][j]);
+            mb |= ((float)o8[j] > 0.f ? 1u : 0u) << j;
+          }
+          const u32x4 ov = __builtin_bit_cast(u32x4, o8);
+          if (out) *reinterpret_cast<u32x4*>(&out[(size_t)c * 8]) = ov;
+          if (rmask) rmask[c] = (uint8_t)mb;
+          *reinterpret_cast<u32x4*>(sp) = ov;  // the next layer's input
+        }
+      }
+      __syncthreads();  // the tile and sAB are complete / free
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+template <typename E>
+struct TBLayer {
+  const E* y;              // ysave of the forward
+  const float* stats;      // [N][6][2]
+  const float* gamma;      // [96]
+  const uint8_t* rmask;    // [N][P][12] ReLU bits of the forward
+  const float* dmask;      // [N][96] or NULL
+  const E* wT;             // [9][96 ci][96 co]; NULL for layer 0 (no input gradient)
+  E* dy;                   // [N][P][96] out: dL/dy (the weight gradient's operand)
+};
+
+template <typename E>
+struct TrunkBwdParams {
+  const E* dout;  // [N][P][96] gradient of the last layer's output
+  E* ws;          // [grid][P][96]: a block's skip gradient between its conv2 and its input
+  float* part;    // [grid][NL][3][96] per-workgroup d gamma, d beta, d bias
+  int NL, N, H, W;
+  TBLayer<E> L[MAXL + 1];
+};
+
+constexpr int DCP = CINP;  // dy tile row stride (elements)
+constexpr int PG = 21;     // pixel groups of the element-wise passes: thread = (pg, c8)
+
+__host__ __device__ inline int tb_dtile_bytes(int P) { return ((P + 1) * DCP * 2 + 15) & ~15; }
+__host__ __device__ constexpr int tb_red_bytes() {  // sRed [PG][3][96] f32, aliased by sW [96][DCP]
+  return PG * 3 * COUT * 4 > COUT * DCP * 2 ? PG * 3 * COUT * 4 : COUT * DCP * 2;
+}
+__host__ __device__ inline size_t tb_lds(int P) { return (size_t)tb_dtile_bytes(P) + tb_red_bytes() + 5 * COUT * 4; }
+
+// Layer i of p.L (forward order: 0 = the stem, 2b+1 / 2b+2 = conv1 / conv2 of block b):
+//   dout_i = dgrad_{i+1} (+ dz_{i+2} when i is even: the block input's skip gradient)
+//   pass 1: dz = (out_i > 0) * dout_i * dmask; sums S1 = sum dz, S2 = sum dz*yhat, S3 = sum yhat
+//   pass 2: dy = rstd*gamma*dz - rstd*mean_g(gamma*dz) - rstd*yhat*mean_g(gamma*dz*yhat)
+//   dgrad (i > 0): dx = sum_tap shift(dy) . W^T[tap], staged in the tile for layer i-1
+template <typename E, int NPT, int NCH>
+__global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_bwd(TrunkBwdParams<E> p) {
+  // no contraction: every expression rounds the same way in the per-layer and the one-launch
+  // kernels (explicit fmaf where a fused multiply-add is wanted), so they agree bitwise
+#pragma clang fp contract(off)
+  typedef typename EV<E>::v8 E8;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int H = p.H, W = p.W, P = H * W;
+  E* sD = reinterpret_cast<E*>(smem);  // [P+1][DCP] (row P = 0): dx -> dz -> dy of each layer
+  float* sRed = reinterpret_cast<float*>(smem + tb_dtile_bytes(P));
+  E* sW = reinterpret_cast<E*>(sRed);  // W^T[tap] as [ci][DCP]
+  float* sCo = reinterpret_cast<float*>(smem + tb_dtile_bytes(P) + tb_red_bytes());  // [3][96]
+  float* sTmp = sCo + 3 * COUT;                                                       // [2][96]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l32 = lane & 31, hh = lane >> 5;
+  const float inv_cnt = 1.0f / (16.0f * (float)P);
+
+  for (int i = threadIdx.x; i < DCP / 8; i += 256) *reinterpret_cast<u32x4*>(&sD[P * DCP + 8 * i]) = u32x4{0u, 0u, 0u, 0u};
+  int qr[NPT], qc[NPT];
+#pragma unroll
+  for (int t = 0; t < NPT; ++t) {
+    const int q = (wave * NPT + t) * 32 + l32;
+    qr[t] = q < P ? q / W : -1000;
+    qc[t] = q < P ? q - qr[t] * W : -1000;
+  }
+  constexpr int NWC = (COUT * C8 + 255) / 256;  // 16-B chunks of one W^T tap per thread
+
+  for (int n = blockIdx.x; n < p.N; n += gridDim.x) {
+    const size_t so = (size_t)n * P * COUT;
+    E* wsl = p.ws + (size_t)blockIdx.x * P * COUT;  // this workgroup's skip-gradient slot
+
+    for (int li = p.NL - 1; li >= 0; --li) {
+      // loop-variant thread coordinates: the per-chunk address math and the taps' row offsets
+      // are recomputed per layer instead of hoisted out of this loop (they would be spilled)
+      const int tid = threadIdx.x + opaque0();
+#pragma unroll
+      for (int t = 0; t < NPT; ++t) asm volatile("" : "+v"(qr[t]), "+v"(qc[t]));
+      const int pg = tid / C8, c8 = tid - pg * C8;
+      const bool gact = tid < PG * C8;
+      const int grp = c8 >> 1;
+      const bool top = li == p.NL - 1;
+      const bool addd = !(li & 1) && li + 2 < p.NL;  // dout += the skip gradient dz_{li+2}
+      const bool keep_dz = !(li & 1) && li >= 2;     // dz of a conv2: the skip gradient of layer li-2
+      float* pp = p.part + ((size_t)blockIdx.x * p.NL + li) * 3 * COUT;
+      float acc_g = 0.f, acc_b = 0.f, acc_bias = 0.f;  // tid < 96: this workgroup's running sums
+      if (tid < COUT && n != blockIdx.x) {
+        acc_g = pp[tid];
+        acc_b = pp[COUT + tid];
+        acc_bias = pp[2 * COUT + tid];
+      }
+      const float* stats = p.L[li].stats;
+      // ---------------- pass 1: dz and per-channel sums ----------------
+      float dm[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dm[j] = 1.f;
+      float mean = 0.f, rstd = 0.f;
+      if (gact) {
+        const float* dmask = p.L[li].dmask;
+        if (dmask) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dm[j] = dmask[(size_t)n * COUT + c8 * 8 + j];
+        }
+        mean = stats[((size_t)n * NGRP + grp) * 2];
+        rstd = stats[((size_t)n * NGRP + grp) * 2 + 1];
+      }
+      const E* yp = p.L[li].y + so;
+      const uint8_t* rmp = p.L[li].rmask + (size_t)n * P * C8;
+      u32x4 yr[NCH];
+      float s1[8], s2[8], s3[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s1[j] = s2[j] = s3[j] = 0.f;
+      constexpr int LB = 7;  // chunks whose loads are in flight together
+#pragma unroll
+      for (int i0 = 0; i0 < NCH; i0 += LB) {
+        u32x4 dv[LB];  // dout (top layer) or the skip gradient (addd): never both
+        uint32_t mv[LB];
+#pragma unroll
+        for (int u = 0; u < LB; ++u) {
+          const int i = i0 + u, px = pg + PG * i;
+          if (i < NCH) yr[i] = u32x4{0u, 0u, 0u, 0u};
+          mv[u] = 0u;
+          dv[u] = u32x4{0u, 0u, 0u, 0u};
+          if (i < NCH && gact && px < P) {
+            const size_t o = (size_t)px * COUT + c8 * 8;
+            if (top) dv[u] = *reinterpret_cast<const u32x4*>(&p.dout[so + o]);
+            else if (addd) dv[u] = *reinterpret_cast<const u32x4*>(&wsl[o]);
+            mv[u] = rmp[px * C8 + c8];
+            yr[i] = *reinterpret_cast<const u32x4*>(&yp[o]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < LB; ++u) {
+          const int i = i0 + u, px = pg + PG * i;
+          if (i < NCH && gact && px < P) {
+            E* sp = &sD[px * DCP + c8 * 8];
+            E8 d8;
+            if (top) {
+              d8 = __builtin_bit_cast(E8, dv[u]);
+            } else {
+              d8 = __builtin_bit_cast(E8, *reinterpret_cast<const u32x4*>(sp));  // dgrad of layer li+1
+              if (addd) {  // + the skip gradient, rounded as the per-layer kernel's dx (+ addend) store
+                const E8 a8 = __builtin_bit_cast(E8, dv[u]);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) d8[j] = (E)((float)d8[j] + (float)a8[j]);
+              }
+            }
+            const E8 y8 = __builtin_bit_cast(E8, yr[i]);
+            const uint32_t pos = mv[u];
+            E8 z8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float d = (float)d8[j] * dm[j];
+              z8[j] = (E)(((pos >> j) & 1u) ? d : 0.f);
+              const float zf = (float)z8[j];
+              const float yh = ((float)y8[j] - mean) * rstd;
+              s1[j] += zf;
+              s2[j] = __builtin_fmaf(zf, yh, s2[j]);
+              s3[j] += yh;
+            }
+            *reinterpret_cast<u32x4*>(sp) = __builtin_bit_cast(u32x4, z8);
+          }
+        }
+      }
+      // tap 0's W^T: loaded here, its latency hidden behind the channel reductions
+      const E* wT = p.L[li].wT;
+      const bool dgrad = li > 0;
+      u32x4 wr[NWC];
+      if (dgrad) {
+#pragma unroll
+        for (int k = 0; k < NWC; ++k) {
+          const int c = tid + 256 * k;
+          if (k < COUT * C8 / 256 || c < COUT * C8) wr[k] = reinterpret_cast<const u32x4*>(wT)[c];
+        }
+      }
+      if (gact) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          sRed[(pg * 3 + 0) * COUT + c8 * 8 + j] = s1[j];
+          sRed[(pg * 3 + 1) * COUT + c8 * 8 + j] = s2[j];
+          sRed[(pg * 3 + 2) * COUT + c8 * 8 + j] = s3[j];
+        }
+      }
+      __syncthreads();
+      float S1 = 0.f, S2 = 0.f, S3 = 0.f, gam = 0.f, cmean = 0.f, crstd = 0.f;
+      if (tid < COUT) {
+        for (int g = 0; g < PG; ++g) {
+          S1 += sRed[(g * 3 + 0) * COUT + tid];
+          S2 += sRed[(g * 3 + 1) * COUT + tid];
+          S3 += sRed[(g * 3 + 2) * COUT + tid];
+        }
+        gam = p.L[li].gamma[tid];
+        cmean = stats[((size_t)n * NGRP + (tid >> 4)) * 2];
+        crstd = stats[((size_t)n * NGRP + (tid >> 4)) * 2 + 1];
+        sTmp[tid] = gam * S1;
+        sTmp[COUT + tid] = gam * S2;
+        acc_g += S2;
+        acc_b += S1;
+      }
+      __syncthreads();
+      if (tid < COUT) {
+        const int g0 = (tid >> 4) * 16;
+        float m1 = 0.f, m2 = 0.f;
+        for (int k = 0; k < 16; ++k) {
+          m1 += sTmp[g0 + k];
+          m2 += sTmp[COUT + g0 + k];
+        }
+        m1 *= inv_cnt;
+        m2 *= inv_cnt;
+        sCo[tid] = crstd * gam;
+        sCo[COUT + tid] = -crstd * crstd * m2;
+        sCo[2 * COUT + tid] = crstd * (crstd * m2 * cmean - m1);
+        acc_bias += crstd * (gam * S1 - (float)P * m1 - m2 * S3);
+        pp[tid] = acc_g;
+        pp[COUT + tid] = acc_b;
+        pp[2 * COUT + tid] = acc_bias;
+      }
+      __syncthreads();
+
+      // tap 0's W^T goes to sW (free now: the sums are read) before pass 2 issues its stores
+      if (dgrad) {
+#pragma unroll
+        for (int k = 0; k < NWC; ++k) {
+          const int c = tid + 256 * k;
+          if (k < COUT * C8 / 256 || c < COUT * C8) {
+            const int ci = c / C8, k8 = c - ci * C8;
+            *reinterpret_cast<u32x4*>(&sW[ci * DCP + k8 * 8]) = wr[k];
+          }
+        }
+      }
+      // ---------------- pass 2: dy (GroupNorm backward) -> LDS tile + HBM ----------------
+      E* dyp = p.L[li].dy + so;
+      if (gact) {
+        float A[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) A[j] = sCo[c8 * 8 + j];
+        const float Bg = sCo[COUT + c8 * 8], Cg = sCo[2 * COUT + c8 * 8];
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) {
+          const int px = pg + PG * i;
+          if (px < P) {
+            E* sp = &sD[px * DCP + c8 * 8];
+            const u32x4 zv = *reinterpret_cast<const u32x4*>(sp);
+            if (keep_dz) *reinterpret_cast<u32x4*>(&wsl[(size_t)px * COUT + c8 * 8]) = zv;
+            const E8 z8 = __builtin_bit_cast(E8, zv);
+            const E8 y8 = __builtin_bit_cast(E8, yr[i]);
+            E8 d8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d8[j] = (E)__builtin_fmaf(A[j], (float)z8[j], __builtin_fmaf(Bg, (float)y8[j], Cg));
+            const u32x4 v = __builtin_bit_cast(u32x4, d8);
+            *reinterpret_cast<u32x4*>(sp) = v;
+            *reinterpret_cast<u32x4*>(&dyp[(size_t)px * COUT + c8 * 8]) = v;
+          }
+        }
+      }
+      if (!dgrad) continue;  // (uniform) the stem's input needs no gradient
+      __syncthreads();
+
+      // ---------------- dgrad: dx = sum_tap shift(dy) . W^T[tap] ----------------
+      f32x16 acc[NPT][3];
+#pragma unroll
+      for (int t = 0; t < NPT; ++t)
+#pragma unroll
+        for (int ct = 0; ct < 3; ++ct)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) acc[t][ct][i] = 0.f;
+      for (int tap = 0; tap < 9; ++tap) {
+        if (tap + 1 < 9) {
+          const u32x4* ws = reinterpret_cast<const u32x4*>(wT + (size_t)(tap + 1) * COUT * COUT);
+#pragma unroll
+          for (int k = 0; k < NWC; ++k) {
+            const int c = tid + 256 * k;
+            if (k < COUT * C8 / 256 || c < COUT * C8) wr[k] = ws[c];
+          }
+        }
+        const int dr = tap / 3 - 1, dc = tap % 3 - 1;
+        int aoff[NPT];
+#pragma unroll
+        for (int t = 0; t < NPT; ++t) {
+          const int sr = qr[t] - dr, sc = qc[t] - dc;
+          const bool v = (unsigned)sr < (unsigned)H && (unsigned)sc < (unsigned)W;
+          aoff[t] = (v ? sr * W + sc : P) * DCP + 8 * hh;
+        }
+        auto ld = [&](int k0, E8 (&a)[NPT], E8 (&b)[3]) {
+#pragma unroll
+          for (int ct = 0; ct < 3; ++ct)
+            b[ct] = *reinterpret_cast<const E8*>(&sW[(ct * 32 + l32) * DCP + k0 + 8 * hh]);
+#pragma unroll
+          for (int t = 0; t < NPT; ++t) a[t] = *reinterpret_cast<const E8*>(&sD[aoff[t] + k0]);
+        };
+        auto mm = [&](const E8 (&a)[NPT], const E8 (&b)[3]) {
+#pragma unroll
+          for (int t = 0; t < NPT; ++t)
+#pragma unroll
+            for (int ct = 0; ct < 3; ++ct) acc[t][ct] = mfma32(a[t], b[ct], acc[t][ct]);
+        };
+        E8 a0[NPT], b0[3], a1[NPT], b1[3];
+        ld(0, a0, b0);
+        __builtin_amdgcn_sched_group_barrier(0x100, NPT + 3, 0);
+#pragma unroll
+        for (int k0 = 0; k0 < COUT; k0 += 32) {
+          ld(k0 + 16, a1, b1);
+          __builtin_amdgcn_sched_group_barrier(0x100, NPT + 3, 0);
+          mm(a0, b0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 3 * NPT, 0);
+          if (k0 + 32 < COUT) {
+            ld(k0 + 32, a0, b0);
+            __builtin_amdgcn_sched_group_barrier(0x100, NPT + 3, 0);
+          }
+          mm(a1, b1);
+          __builtin_amdgcn_sched_group_barrier(0x008, 3 * NPT, 0);
+        }
+        __syncthreads();  // sW (and, after the last tap, sD) fully read
+        if (tap + 1 < 9) {
+#pragma unroll
+          for (int k = 0; k < NWC; ++k) {
+            const int c = tid + 256 * k;
+            if (k < COUT * C8 / 256 || c < COUT * C8) {
+              const int ci = c / C8, k8 = c - ci * C8;
+              *reinterpret_cast<u32x4*>(&sW[ci * DCP + k8 * 8]) = wr[k];
+            }
+          }
+          __syncthreads();
+        }
+      }
+      // dx -> the tile (16-bit, as the per-layer kernel's dx store): layer li-1's dout
+#pragma unroll
+      for (int t = 0; t < NPT; ++t)
+#pragma unroll
+        for (int ct = 0; ct < 3; ++ct)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int px = (wave * NPT + t) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+            if (px < P) sD[px * DCP + ct * 32 + l32] = (E)acc[t][ct][i];
+          }
+      __syncthreads();
+    }
+  }
+}
+
+// out[i] = sum_g part[g * n + i] in fixed order (k_reduce of mscnn_bwd.hip, small n)
+__global__ __launch_bounds__(256) void k_reduce_rows(const float* __restrict__ part, int G, int n, float* __restrict__ out) {
+  constexpr int S = 16, IB = 256 / S;
+  __shared__ float sp[S][IB];
+  const int li = threadIdx.x % IB, s = threadIdx.x / IB;
+  const int i = blockIdx.x * IB + li;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (i < n) {
+    int g = s;
+    for (; g + 3 * S < G; g += 4 * S) {
+      a0 += part[(int64_t)g * n + i];
+      a1 += part[(int64_t)(g + S) * n + i];
+      a2 += part[(int64_t)(g + 2 * S) * n + i];
+      a3 += part[(int64_t)(g + 3 * S) * n + i];
+    }
+    for (; g < G; g += S) a0 += part[(int64_t)g * n + i];
+  }
+  sp[s][li] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (s == 0 && i < n) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < S; ++k) t += sp[k][li];
+    out[i] = t;
+  }
+}
+
+int trunk_grid(int n, size_t lds) {
+  const int per_cu = lds <= 80 * 1024 ? 2 : 1;
+  const int cap = per_cu * num_cus();
+  return n < cap ? n : cap;
+}
+
+template <typename K>
+void lds_attr_once(K kernel, bool& done) {
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    done = true;
+  }
+}
+
+int launched(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof g_err, "%s launch: %s", what, hipGetErrorString(e));
+    return MS_EHIP;
+  }
+  return MS_OK;
+}
+
+template <typename E, int NPT, bool FULL>
+int launch_trunk_fwd(const TrunkFwdParams<E>& p, hipStream_t s) {
+  static bool attr = false;
+  lds_attr_once(k_trunk_fwd<E, NPT, FULL>, attr);
+  const size_t lds = tf_lds(p.H * p.W);
+  hipLaunchKernelGGL((k_trunk_fwd<E, NPT, FULL>), dim3(trunk_grid(p.N, lds)), dim3(256), lds, s, p);
+  return launched("k_trunk_fwd");
+}
+
+template <typename E>
+int run_trunk_fwd(const uint16_t* x0, const mc_fwd_layer* layers, int nl, void* work, int n, int h, int w,
+                  float eps, hipStream_t s) {
+  TrunkFwdParams<E> p;
+  memset(&p, 0, sizeof p);
+  p.x0 = reinterpret_cast<const E*>(x0);
+  p.ws = reinterpret_cast<E*>(work);
+  p.NL = nl;
+  p.N = n;
+  p.H = h;
+  p.W = w;
+  p.eps = eps;
+  for (int l = 0; l < nl; ++l) {
+    const mc_fwd_layer& a = layers[l];
+    p.L[l].wt = reinterpret_cast<const E*>(a.w);
+    p.L[l].bias = a.bias;
+    p.L[l].gamma = a.gamma;
+    p.L[l].beta = a.beta;
+    p.L[l].dmask = a.dmask;
+    p.L[l].out = reinterpret_cast<E*>(a.out);
+    p.L[l].ysave = reinterpret_cast<E*>(a.ysave);
+    p.L[l].stats = a.stats;
+    p.L[l].rmask = a.relu_mask;
+  }
+  const int P = h * w;
+  if (P == 256) return launch_trunk_fwd<E, 2, true>(p, s);
+  const int npt = ((P + 31) / 32 + WAVES - 1) / WAVES;
+  switch (npt) {
+    case 1: return launch_trunk_fwd<E, 1, false>(p, s);
+    case 2: return launch_trunk_fwd<E, 2, false>(p, s);
+    case 3: return launch_trunk_fwd<E, 3, false>(p, s);
+    default: return launch_trunk_fwd<E, 4, false>(p, s);
+  }
+}
+
+template <typename E, int NPT, int NCH>
+int launch_trunk_bwd(const TrunkBwdParams<E>& p, int grid, hipStream_t s) {
+  static bool attr = false;
+  lds_attr_once(k_trunk_bwd<E, NPT, NCH>, attr);
+  hipLaunchKernelGGL((k_trunk_bwd<E, NPT, NCH>), dim3(grid), dim3(256), tb_lds(p.H * p.W), s, p);
+  return launched("k_trunk_bwd");
+}
+
+template <typename E>
+int run_trunk_bwd(const uint16_t* dout, const mc_bwd_layer* layers, int nl, float* dgn, void* work, int n, int h,
+                  int w, hipStream_t s) {
+  const int P = h * w;
+  const int grid = trunk_grid(n, tb_lds(P));
+  TrunkBwdParams<E> p;
+  memset(&p, 0, sizeof p);
+  p.dout = reinterpret_cast<const E*>(dout);
+  p.ws = reinterpret_cast<E*>(work);
+  p.part = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(work) + (size_t)grid * P * COUT * 2);
+  p.NL = nl;
+  p.N = n;
+  p.H = h;
+  p.W = w;
+  for (int l = 0; l < nl; ++l) {
+    const mc_bwd_layer& a = layers[l];
+    p.L[l].y = reinterpret_cast<const E*>(a.ysave);
+    p.L[l].stats = a.stats;
+    p.L[l].gamma = a.gamma;
+    p.L[l].rmask = a.relu_mask;
+    p.L[l].dmask = a.dmask;
+    p.L[l].wT = reinterpret_cast<const E*>(a.wT);
+    p.L[l].dy = reinterpret_cast<E*>(a.dy);
+  }
+  int rc;
+  if (P <= 128) rc = launch_trunk_bwd<E, 1, 13>(p, grid, s);
+  else if (P <= 256) rc = launch_trunk_bwd<E, 2, 13>(p, grid, s);
+  else if (P <= 384) rc = launch_trunk_bwd<E, 3, 25>(p, grid, s);
+  else rc = launch_trunk_bwd<E, 4, 25>(p, grid, s);
+  if (rc) return rc;
+  const int nout = nl * 3 * COUT;
+  hipLaunchKernelGGL(k_reduce_rows, dim3((unsigned)((nout + 15) / 16)), dim3(256), 0, s, p.part, grid, nout, dgn);
+  return launched("k_reduce_rows");
+}
+
+bool trunk_shape_ok(int n, int h, int w, int nl, int max_nl, const char* what) {
+  if (n <= 0 || h <= 0 || w <= 0 || nl <= 0 || nl > max_nl) {
+    snprintf(g_err, sizeof g_err, "%s: bad sizes (n %d, board %dx%d, %d layers; at most %d)", what, n, h, w, nl, max_nl);
+    return false;
+  }
+  if (h * w > 512 || w > 64) {
+    snprintf(g_err, sizeof g_err, "%s: board %dx%d unsupported (at most 512 cells)", what, h, w);
+    return false;
+  }
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t mc_trunk_fwd_workspace(int32_t n, int32_t h, int32_t w_) {
+  if (n <= 0 || h <= 0 || w_ <= 0 || h * w_ > 512) return -1;
+  const int P = h * w_;
+  return (int64_t)trunk_grid(n, tf_lds(P)) * P * COUT * 2;
+}
+
+int mc_trunk_fwd(const uint16_t* x0, const mc_fwd_layer* layers, int32_t nlayers, void* work, int64_t work_bytes,
+                 int32_t n, int32_t h, int32_t w_, float eps, int32_t dtype, void* stream) {
+  if (!trunk_shape_ok(n, h, w_, nlayers, MAXL, "mc_trunk_fwd")) return MS_EINVAL;
+  if (!x0 || !layers || (nlayers & 1)) {
+    snprintf(g_err, sizeof g_err, "mc_trunk_fwd: bad argument (x0, layers, or an odd layer count %d)", nlayers);
+    return MS_EINVAL;
+  }
+  for (int l = 0; l < nlayers; ++l) {
+    const mc_fwd_layer& a = layers[l];
+    if (!a.w || !a.bias || !a.gamma || !a.beta) {
+      snprintf(g_err, sizeof g_err, "mc_trunk_fwd: layer %d lacks weights or GroupNorm parameters", l);
+      return MS_EINVAL;
+    }
+    if ((l & 1) && a.dmask) {
+      snprintf(g_err, sizeof g_err, "mc_trunk_fwd: layer %d is a conv2 (no dropout)", l);
+      return MS_EINVAL;
+    }
+  }
+  if (!layers[nlayers - 1].out) {
+    snprintf(g_err, sizeof g_err, "mc_trunk_fwd: the last layer's out is required");
+    return MS_EINVAL;
+  }
+  const int64_t need = mc_trunk_fwd_workspace(n, h, w_);
+  bool need_ws = false;
+  for (int l = 1; l + 2 < nlayers; l += 2) need_ws |= layers[l].out == nullptr;
+  if (need_ws && (!work || work_bytes < need)) {
+    snprintf(g_err, sizeof g_err, "mc_trunk_fwd: workspace %lld < %lld bytes", (long long)work_bytes, (long long)need);
+    return MS_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MC_DT_BF16) return run_trunk_fwd<__bf16>(x0, layers, nlayers, work, n, h, w_, eps, s);
+  if (dtype == MC_DT_F16) return run_trunk_fwd<_Float16>(x0, layers, nlayers, work, n, h, w_, eps, s);
+  snprintf(g_err, sizeof g_err, "mc_trunk_fwd: dtype %d unsupported (0 bf16, 1 f16)", dtype);
+  return MS_EINVAL;
+}
+
+int64_t mc_trunk_bwd_workspace(int32_t nlayers, int32_t n, int32_t h, int32_t w_) {
+  if (n <= 0 || h <= 0 || w_ <= 0 || h * w_ > 512 || nlayers <= 0 || nlayers > MAXL + 1) return -1;
+  const int P = h * w_;
+  const int64_t grid = trunk_grid(n, tb_lds(P));
+  return grid * P * COUT * 2 + grid * nlayers * 3 * COUT * 4;
+}
+
+int mc_trunk_bwd(const uint16_t* dout, const mc_bwd_layer* layers, int32_t nlayers, float* dgn, void* work,
+                 int64_t work_bytes, int32_t n, int32_t h, int32_t w_, int32_t dtype, void* stream) {
+  if (!trunk_shape_ok(n, h, w_, nlayers, MAXL + 1, "mc_trunk_bwd")) return MS_EINVAL;
+  if (!dout || !layers || !dgn || !work || !(nlayers & 1)) {
+    snprintf(g_err, sizeof g_err, "mc_trunk_bwd: bad argument (dout, layers, dgn, work, or an even layer count %d)",
+             nlayers);
+    return MS_EINVAL;
+  }
+  for (int l = 0; l < nlayers; ++l) {
+    const mc_bwd_layer& a = layers[l];
+    if (!a.ysave || !a.stats || !a.gamma || !a.relu_mask || !a.dy || ((l == 0) != (a.wT == nullptr))) {
+      snprintf(g_err, sizeof g_err, "mc_trunk_bwd: layer %d: ysave, stats, gamma, relu_mask, dy required; wT iff l > 0", l);
+      return MS_EINVAL;
+    }
+    if (l > 0 && !(l & 1) && a.dmask) {
+      snprintf(g_err, sizeof g_err, "mc_trunk_bwd: layer %d is a conv2 (no dropout)", l);
+      return MS_EINVAL;
+    }
+  }
+  const int64_t need = mc_trunk_bwd_workspace(nlayers, n, h, w_);
+  if (work_bytes < need) {
+    snprintf(g_err, sizeof g_err, "mc_trunk_bwd: workspace %lld < %lld bytes", (long long)work_bytes, (long long)need);
+    return MS_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MC_DT_BF16) return run_trunk_bwd<__bf16>(dout, layers, nlayers, dgn, work, n, h, w_, s);
+  if (dtype == MC_DT_F16) return run_trunk_bwd<_Float16>(dout, layers, nlayers, dgn, work, n, h, w_, s);
+  snprintf(g_err, sizeof g_err, "mc_trunk_bwd: dtype %d unsupported (0 bf16, 1 f16)", dtype);
+  return MS_EINVAL;
+}
+
+}  // extern "C"

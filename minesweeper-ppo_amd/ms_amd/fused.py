@@ -9,6 +9,7 @@ autocast, the reference's training precision, ppo.py:25); weights are re-laid ou
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -50,10 +51,10 @@ VARIANT_FWD, VARIANT_BWD, VARIANT_WGRAD = 0, 1, 2  # mc_set_variant kernels (inc
 
 
 class kernel_variant:
-    """Context manager: run mc_conv_gn_fwd (kernel 0) or mc_conv_gn_bwd (kernel 1) on one variant
-    -- 0 the dispatcher's choice, 1 the per-sample kernel, 2 / 3 the pixel-split wave-specialised
-    kernels, 4 / 5 the channel-split forward (include/msenv_debug.h) -- for parity tests of every
-    path and same-process A/B timing."""
+    """Context manager: run one kernel variant (include/msenv_debug.h mc_set_variant) -- for the
+    weight gradient (kernel 2) 0 = the default, 1 / 2 = k_wgrad, 3 = k_wgrad_c96; the forward and
+    data backward (kernels 0 / 1) have only the per-sample kernel (0 = 1) since round 5 -- for
+    parity tests of every path and same-process A/B timing."""
 
     def __init__(self, kernel: int, variant: int):
         self.kernel, self.variant = kernel, variant
@@ -243,9 +244,169 @@ def trunk_layers(model) -> list:
     return layers
 
 
+# ------------------------------------------------------------------------------------
+# The residual stack in one launch per direction (csrc/mscnn_trunk.hip, include/mscnn.h
+# mc_trunk_fwd / mc_trunk_bwd): bitwise the per-layer path, without the per-layer HBM round
+# trips of the activations. ``CHAIN`` selects it (the default);
+# ``chain_path(False)`` runs the per-layer kernels, for parity tests and A/B timing.
+
+CHAIN = os.environ.get("MS_TRUNK_CHAIN", "1") != "0"  # MS_TRUNK_CHAIN=0: per-layer kernels (A/B runs)
+MAX_CHAIN_LAYERS = 16  # MC_TRUNK_MAX_LAYERS
+
+
+class chain_path:
+    """Context manager: run the trunk through the one-launch kernels (True) or per layer (False)."""
+
+    def __init__(self, on: bool):
+        self.on = on
+
+    def __enter__(self):
+        global CHAIN
+        self.prev, CHAIN = CHAIN, self.on
+        return self
+
+    def __exit__(self, *exc):
+        global CHAIN
+        CHAIN = self.prev
+        return False
+
+
+class _FwdLayer(ctypes.Structure):  # mc_fwd_layer
+    _fields_ = [(n, _vp) for n in ("w", "bias", "gamma", "beta", "dmask", "out", "ysave", "stats", "relu_mask")]
+
+
+class _BwdLayer(ctypes.Structure):  # mc_bwd_layer
+    _fields_ = [(n, _vp) for n in ("ysave", "stats", "gamma", "relu_mask", "dmask", "wT", "dy")]
+
+
+_tf = _tfws = _tb = _tbws = _wg = None
+
+
+def _trunk_bind():
+    global _tf, _tfws, _tb, _tbws, _wg
+    if _tf is None:
+        _tf = _fn("mc_trunk_fwd", [_vp, ctypes.POINTER(_FwdLayer), _i32, _vp, ctypes.c_int64] + [_i32] * 3
+                  + [_f32, _i32, _vp])
+        _tfws = _fn("mc_trunk_fwd_workspace", [_i32] * 3)
+        _tfws.restype = ctypes.c_int64
+        _tb = _fn("mc_trunk_bwd", [_vp, ctypes.POINTER(_BwdLayer), _i32, _vp, _vp, ctypes.c_int64] + [_i32] * 4
+                  + [_vp])
+        _tbws = _fn("mc_trunk_bwd_workspace", [_i32] * 4)
+        _tbws.restype = ctypes.c_int64
+        _wg = _fn("mc_conv_wgrad", [_vp] * 4 + [ctypes.c_int64] + [_i32] * 5 + [_vp])
+
+
+def chain_ok(layers, H: int, W: int) -> bool:
+    """The one-launch trunk takes 96-channel residual stacks of at most 8 blocks on boards of
+    at most 512 cells (the per-layer kernels' range)."""
+    nres = len(layers) - 1
+    return CHAIN and 0 < nres <= MAX_CHAIN_LAYERS and nres % 2 == 0 and H * W <= 512 and W <= 64
+
+
+def trunk_forward_chain(x, layers, H: int, W: int, dmasks, save: bool):
+    """Residual stack (layers[1:]) on the stem output ``x`` [N, P, 96] in one mc_trunk_fwd.
+    Returns (out, outs, ys, sts, rms): per layer lists of the saved tensors (empty unless ``save``)."""
+    _trunk_bind()
+    n, p, c = x.shape
+    assert c == COUT and x.is_contiguous() and p == H * W
+    dev, et = x.device, x.dtype
+    res = layers[1:]
+    nl = len(res)
+    arr = (_FwdLayer * nl)()
+    keep = []  # f32 parameter copies must outlive the enqueue (the allocator may reuse their memory only after)
+    outs, ys, sts, rms = [], [], [], []
+    eps = res[0][1].eps
+    for k, (conv, norm) in enumerate(res):
+        assert norm.eps == eps and conv.weight.shape[0] == COUT and conv.weight.shape[1] == COUT
+        f32c = lambda t: t.detach().to(torch.float32).contiguous()  # noqa: E731
+        b, g, be = f32c(conv.bias), f32c(norm.weight), f32c(norm.bias)
+        dm = None
+        if k % 2 == 0 and dmasks is not None:  # conv1 of block k // 2: Dropout2d after its ReLU
+            dm = dmasks[k // 2].to(torch.float32).contiguous()
+            assert dm.shape == (n, COUT)
+        last = k == nl - 1
+        out = torch.empty((n, p, COUT), dtype=et, device=dev) if (save or last) else None
+        y = torch.empty((n, p, COUT), dtype=et, device=dev) if save else None
+        st = torch.empty((n, NGROUPS, 2), dtype=torch.float32, device=dev) if save else None
+        rm = torch.empty((n, p, COUT // 8), dtype=torch.uint8, device=dev) if save else None
+        keep += [b, g, be, dm]
+        if save:
+            outs.append(out)
+            ys.append(y)
+            sts.append(st)
+            rms.append(rm)
+        arr[k] = _FwdLayer(L.ptr(_packed(conv.weight, "f", et, COUT)), L.ptr(b), L.ptr(g), L.ptr(be), L.ptr(dm),
+                           L.ptr(out), L.ptr(y), L.ptr(st), L.ptr(rm))
+        if last:
+            final = out
+    nws = int(_tfws(n, H, W))
+    work = None if save else torch.empty(max(nws, 0), dtype=torch.uint8, device=dev)
+    _check(_tf(L.ptr(x), arr, nl, L.ptr(work), 0 if work is None else work.numel(), n, H, W, eps, _dt(x),
+               L.stream_ptr(dev)))
+    return final, outs, ys, sts, rms
+
+
+def trunk_backward_chain(dout, layers, ys, sts, rms, dmasks, H: int, W: int):
+    """GroupNorm + data backward of the stem (layers[0]) and the residual stack in one
+    mc_trunk_bwd. Returns (dys, dgn): per layer dL/dy [N, P, 96] and d gamma / d beta / d bias f32
+    [nlayers, 3, 96]."""
+    _trunk_bind()
+    n, p, _ = dout.shape
+    dev, et = dout.device, dout.dtype
+    nl = len(layers)
+    arr = (_BwdLayer * nl)()
+    keep, dys = [], []
+    for li, (conv, norm) in enumerate(layers):
+        g = norm.weight.detach().to(torch.float32).contiguous()
+        dm = None
+        if li % 2 == 1 and dmasks is not None:
+            dm = dmasks[(li - 1) // 2].to(torch.float32).contiguous()
+        wT = _packed(conv.weight, "t", et) if li > 0 else None
+        dy = torch.empty((n, p, COUT), dtype=et, device=dev)
+        keep += [g, dm]
+        dys.append(dy)
+        arr[li] = _BwdLayer(L.ptr(ys[li]), L.ptr(sts[li]), L.ptr(g), L.ptr(rms[li]), L.ptr(dm), L.ptr(wT), L.ptr(dy))
+    dgn = torch.empty((nl, 3, COUT), dtype=torch.float32, device=dev)
+    nws = int(_tbws(nl, n, H, W))
+    if nws < 0:
+        raise L.MsEnvError("mc_trunk_bwd_workspace: bad sizes")
+    work = torch.empty(nws, dtype=torch.uint8, device=dev)
+    _check(_tb(L.ptr(dout), arr, nl, L.ptr(dgn), L.ptr(work), nws, n, H, W, _dt(dout), L.stream_ptr(dev)))
+    return dys, dgn
+
+
+def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, H: int, W: int) -> torch.Tensor:
+    """Weight gradient f32 [9, 96, cin] (tap, co, ci) of a conv3x3 layer from dL/dy and its input
+    (mc_conv_wgrad; mc_conv_gn_bwd's second half)."""
+    _trunk_bind()
+    global _bwd_ws
+    if _bwd_ws is None:
+        _bwd_ws = _fn("mc_conv_gn_bwd_workspace", [_i32] * 4)
+        _bwd_ws.restype = ctypes.c_int64
+    n, p, cin = x.shape
+    assert dy.shape == (n, p, COUT) and dy.dtype == x.dtype and x.is_contiguous() and dy.is_contiguous()
+    dw = torch.empty((9, COUT, cin), dtype=torch.float32, device=x.device)
+    nws = int(_bwd_ws(n, H, W, cin))
+    work = torch.empty(nws, dtype=torch.float32, device=x.device)
+    _check(_wg(L.ptr(dy), L.ptr(x), L.ptr(dw), L.ptr(work), nws, n, H, W, cin, _dt(x), L.stream_ptr(x.device)))
+    return dw
+
+
 def _trunk_forward(x0, layers, H, W, dmasks, save):
     """Runs every layer; with ``save`` returns the tensors the backward needs:
     acts[l] = input of layer l (acts[l + 1] = its output), ys[l], sts[l], and the ReLU bitmasks."""
+    if chain_ok(layers, H, W):
+        conv, norm = layers[0]
+        wt = _packed(conv.weight, "f", x0.dtype, x0.shape[-1])
+        if save:
+            x, y, st, rm = conv_gn_fwd(x0, wt, conv.bias, norm.weight, norm.bias, H, W, save=True, eps=norm.eps,
+                                       want_mask=True)
+        else:
+            x, _, _ = conv_gn_fwd(x0, wt, conv.bias, norm.weight, norm.bias, H, W, save=False, eps=norm.eps)
+        out, outs, ys, sts, rms = trunk_forward_chain(x, layers, H, W, dmasks, save)
+        if not save:
+            return out, [], [], [], []
+        return out, [x0, x] + outs, [y] + ys, [st] + sts, [rm] + rms
     acts, ys, sts, rms = [x0], [], [], []
     x, blk_in = x0, None
     for li, (conv, norm) in enumerate(layers):
@@ -272,6 +433,7 @@ def _trunk_forward(x0, layers, H, W, dmasks, save):
 class _TrunkFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x0, H, W, dmasks, layers, *params):
+        ctx.chain = chain_ok(layers, H, W)  # the backward takes the path the forward took
         out, acts, ys, sts, rms = _trunk_forward(x0, layers, H, W, dmasks, save=True)
         ctx.H, ctx.W, ctx.layers, ctx.dmasks = H, W, layers, dmasks
         ctx.saved = (acts, ys, sts, rms)
@@ -285,6 +447,17 @@ class _TrunkFn(torch.autograd.Function):
         grads = {}
         d = dout.to(acts[0].dtype).contiguous()
         nl = len(layers)
+        if ctx.chain:
+            dys, dgn = trunk_backward_chain(d, layers, ys, sts, rms, dmasks, H, W)
+            ctx.saved = None
+            out = [None, None, None, None, None]
+            for li, (conv, norm) in enumerate(layers):
+                dw = conv_wgrad(dys[li], acts[li], H, W)
+                dys[li] = None
+                gs = (dw_to_conv(dw, conv.weight.shape[1]), dgn[li, 2], dgn[li, 0], dgn[li, 1])
+                for p, g in zip((conv.weight, conv.bias, norm.weight, norm.bias), gs):
+                    out.append(g.to(p.dtype) if p.requires_grad else None)
+            return tuple(out)
         skip = None  # dz of a block's second half: the block input's skip gradient
         for li in range(nl - 1, -1, -1):
             conv, norm = layers[li]

@@ -68,6 +68,52 @@ def test_cnn_entry_points_validate_arguments():
     assert b"dtype 7" in lib.mc_last_error()
 
 
+def test_trunk_entry_points_validate_arguments():
+    """mc_trunk_fwd / mc_trunk_bwd / mc_conv_wgrad refuse bad layer lists and sizes before
+    anything touches the device (the fake pointers are never dereferenced)."""
+    from ms_amd import _lib as L
+    from ms_amd import fused as F
+    lib = L.load()
+    lib.mc_last_error.restype = ctypes.c_char_p
+    F._trunk_bind()
+    fake = ctypes.c_void_p(4096)
+    arr = (F._FwdLayer * 2)()
+    assert F._tf(fake, arr, 1, None, 0, 4, 16, 16, 1e-5, 1, None) != 0  # odd layer count
+    assert F._tf(fake, arr, 2, None, 0, 4, 16, 16, 1e-5, 1, None) != 0  # layer 0 has no weights
+    assert b"layer 0" in lib.mc_last_error()
+    for k in range(2):
+        arr[k] = F._FwdLayer(4096, 4096, 4096, 4096, None, None, None, None, None)
+    assert F._tf(fake, arr, 2, None, 0, 4, 16, 16, 1e-5, 1, None) != 0  # the last layer's out is required
+    assert b"last layer" in lib.mc_last_error()
+    arr[1] = F._FwdLayer(4096, 4096, 4096, 4096, 4096, 4096, None, None, None)
+    assert F._tf(fake, arr, 2, None, 0, 4, 16, 16, 1e-5, 1, None) != 0  # dropout on a conv2
+    assert F._tf(fake, arr, 17, None, 0, 4, 16, 16, 1e-5, 1, None) != 0  # > MC_TRUNK_MAX_LAYERS
+    barr = (F._BwdLayer * 3)()
+    assert F._tb(fake, barr, 2, fake, fake, 1 << 30, 4, 16, 16, 1, None) != 0  # even layer count
+    assert F._tb(fake, barr, 3, fake, fake, 1 << 30, 4, 16, 16, 1, None) != 0  # empty layers
+    assert b"layer 0" in lib.mc_last_error()
+    barr[0] = F._BwdLayer(4096, 4096, 4096, 4096, None, 4096, 4096)  # the stem takes no wT
+    assert F._tb(fake, barr, 3, fake, fake, 1 << 30, 4, 16, 16, 1, None) != 0
+    assert F._tfws(4, 40, 40) < 0 and F._tbws(3, 4, 40, 40) < 0  # boards of more than 512 cells
+    assert F._wg(fake, fake, fake, fake, 1 << 30, 4, 16, 16, 32, 1, None) != 0  # cin 16 or 96 only
+    assert b"mc_conv_wgrad" in lib.mc_last_error()
+
+
+def test_set_variant_validates_each_kernel_range():
+    """mc_set_variant refuses a variant a kernel does not have (4 / 5 used to be
+    accepted for every kernel and silently ran another kernel than the one named)."""
+    from ms_amd import _lib as L
+    lib = L.load()
+    sv = lib.mc_set_variant
+    sv.argtypes = [ctypes.c_int32, ctypes.c_int32]
+    for kernel, vmax in ((0, 1), (1, 1), (2, 3)):
+        for v in range(vmax + 1):
+            assert sv(kernel, v) == 0
+        assert sv(kernel, vmax + 1) != 0 and sv(kernel, -1) != 0
+        assert sv(kernel, 0) == 0
+    assert sv(3, 0) != 0
+
+
 def test_single_hip_runtime_mapped():
     from ms_amd import _lib as L
     L.load()

@@ -18,10 +18,13 @@ ap.add_argument("--channels-last", action="store_true")
 ap.add_argument("--benchmark", action="store_true")
 ap.add_argument("--amp", default="fp16")
 ap.add_argument("--fwd-only", action="store_true")
+ap.add_argument("--chain", type=int, default=1, help="one-launch trunk (1) or per-layer kernels (0)")
 ap.add_argument("--pure-bf16", action="store_true", help="model + obs in bf16, no autocast (timing only)")
 args = ap.parse_args()
 torch.backends.cudnn.benchmark = args.benchmark
+from ms_amd import fused as _F  # noqa: E402
 from ms_amd.models import build_model  # noqa: E402
+_F.CHAIN = bool(args.chain)
 from ms_amd.ppo import PPOConfig, ppo_update  # noqa: E402
 from ms_amd.buffers import Batch  # noqa: E402
 

@@ -380,8 +380,9 @@ template <typename E>
 struct TrunkBwdParams {
   const E* dout;  // [N][P][96] gradient of the last layer's output
   E* ws;          // [grid][P][96]: a block's skip gradient between its conv2 and its input
-  float* part;    // [grid][NL][3][96] per-workgroup d gamma, d beta, d bias
+  float* part;    // [VG][NL][3][96] d gamma, d beta, d bias per partial row
   int NL, N, H, W;
+  int VG;         // partial rows: the per-layer kernel's grid (min(N, 2 x CUs)), so the sums match it
   TBLayer<E> L[MAXL + 1];
 };
 
@@ -425,7 +426,10 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_bwd(TrunkBwdPar
   }
   constexpr int NWC = (COUT * C8 + 255) / 256;  // 16-B chunks of one W^T tap per thread
 
-  for (int n = blockIdx.x; n < p.N; n += gridDim.x) {
+  // partial row vb takes samples vb, vb + VG, ... in order, as workgroup vb of the per-layer
+  // kernel does; a workgroup runs rows blockIdx.x, blockIdx.x + gridDim.x, ... (VG >= gridDim.x)
+  for (int vb = blockIdx.x; vb < p.VG; vb += gridDim.x)
+  for (int n = vb; n < p.N; n += p.VG) {
     const size_t so = (size_t)n * P * COUT;
     E* wsl = p.ws + (size_t)blockIdx.x * P * COUT;  // this workgroup's skip-gradient slot
 
@@ -441,9 +445,9 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_bwd(TrunkBwdPar
       const bool top = li == p.NL - 1;
       const bool addd = !(li & 1) && li + 2 < p.NL;  // dout += the skip gradient dz_{li+2}
       const bool keep_dz = !(li & 1) && li >= 2;     // dz of a conv2: the skip gradient of layer li-2
-      float* pp = p.part + ((size_t)blockIdx.x * p.NL + li) * 3 * COUT;
-      float acc_g = 0.f, acc_b = 0.f, acc_bias = 0.f;  // tid < 96: this workgroup's running sums
-      if (tid < COUT && n != blockIdx.x) {
+      float* pp = p.part + ((size_t)vb * p.NL + li) * 3 * COUT;
+      float acc_g = 0.f, acc_b = 0.f, acc_bias = 0.f;  // tid < 96: this partial row's running sums
+      if (tid < COUT && n != vb) {
         acc_g = pp[tid];
         acc_b = pp[COUT + tid];
         acc_bias = pp[2 * COUT + tid];
@@ -729,6 +733,8 @@ int trunk_grid(int n, size_t lds) {
   const int cap = per_cu * num_cus();
   return n < cap ? n : cap;
 }
+// the backward's partial rows: mscnn_bwd.hip make_plan's grid_d
+int trunk_vgrid(int n) { return n < 2 * num_cus() ? n : 2 * num_cus(); }
 
 template <typename K>
 void lds_attr_once(K kernel, bool& done) {
@@ -809,6 +815,7 @@ int run_trunk_bwd(const uint16_t* dout, const mc_bwd_layer* layers, int nl, floa
   p.dout = reinterpret_cast<const E*>(dout);
   p.ws = reinterpret_cast<E*>(work);
   p.part = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(work) + (size_t)grid * P * COUT * 2);
+  p.VG = trunk_vgrid(n);
   p.NL = nl;
   p.N = n;
   p.H = h;
@@ -830,7 +837,7 @@ int run_trunk_bwd(const uint16_t* dout, const mc_bwd_layer* layers, int nl, floa
   else rc = launch_trunk_bwd<E, 4, 25>(p, grid, s);
   if (rc) return rc;
   const int nout = nl * 3 * COUT;
-  hipLaunchKernelGGL(k_reduce_rows, dim3((unsigned)((nout + 15) / 16)), dim3(256), 0, s, p.part, grid, nout, dgn);
+  hipLaunchKernelGGL(k_reduce_rows, dim3((unsigned)((nout + 15) / 16)), dim3(256), 0, s, p.part, p.VG, nout, dgn);
   return launched("k_reduce_rows");
 }
 
@@ -896,7 +903,7 @@ int64_t mc_trunk_bwd_workspace(int32_t nlayers, int32_t n, int32_t h, int32_t w_
   if (n <= 0 || h <= 0 || w_ <= 0 || h * w_ > 512 || nlayers <= 0 || nlayers > MAXL + 1) return -1;
   const int P = h * w_;
   const int64_t grid = trunk_grid(n, tb_lds(P));
-  return grid * P * COUT * 2 + grid * nlayers * 3 * COUT * 4;
+  return grid * P * COUT * 2 + (int64_t)trunk_vgrid(n) * nlayers * 3 * COUT * 4;
 }
 
 int mc_trunk_bwd(const uint16_t* dout, const mc_bwd_layer* layers, int32_t nlayers, float* dgn, void* work,

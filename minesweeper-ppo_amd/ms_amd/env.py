@@ -277,6 +277,10 @@ class VecMinesweeper:
         codes = out.get("codes") if out is not None else None
         if codes is not None:  # the rollout buffer's u8 cell codes instead of the f32 obs (ms_step_codes)
             assert codes.dtype == torch.uint8 and codes.is_contiguous() and codes.numel() == n * self.H * self.W
+            if out.get("obs") is not None:
+                raise ValueError("step(out=...): give either 'obs' or 'codes', not both (codes replace the obs)")
+            if self.as_numpy:
+                raise ValueError("step(out=...): 'codes' is a device-buffer path; it cannot be used with as_numpy=True")
             a = a.to(torch.int64)
         if out is not None:
             obs, mask = out.get("obs"), out["action_mask"]
@@ -298,7 +302,8 @@ class VecMinesweeper:
                        L.ptr(step), L.ptr(last_new), L.ptr(frac), L.ptr(outcome), self._stream()))
         self._version += 1
         infos = _LazyInfos(step, last_new, frac, outcome, dones)
-        batch = self._host({"obs": obs, "action_mask": mask})
+        batch = {"obs": obs, "action_mask": mask} if codes is None else {"codes": codes, "action_mask": mask}
+        batch = self._host(batch)
         if self.as_numpy:
             return batch, rewards.cpu().numpy(), dones.cpu().numpy(), infos
         return batch, rewards, dones, infos

@@ -71,7 +71,8 @@ class _ResidualBlock(nn.Module):
     def forward(self, x: torch.Tensor, dmask: Optional[torch.Tensor] = None) -> torch.Tensor:
         y = self.act(self.norm1(self.conv1(x)))
         # dmask: keyed Dropout2d mask [N, C] (keep / (1 - p)), in place of the torch-RNG draw
-        # (the scale multiplies in f32 and only the product is rounded, as nn.Dropout2d does)
+        # (y is f32 here: group_norm is on autocast's fp32 list, so this is nn.Dropout2d's f32
+        # product; for a 16-bit y ATen would round the 1/(1-p) scale to y's dtype first)
         y = (y.float() * dmask.float()[:, :, None, None]).to(y.dtype) if dmask is not None else self.dropout(y)
         y = self.norm2(self.conv2(y))
         return self.act(y + x)
@@ -216,6 +217,8 @@ class CNNPolicy(nn.Module):
 def build_model(name: str, *, obs_shape: tuple[int, int, int], env_overrides: Dict[str, bool] | None = None,
                 model_cfg: Optional[dict] = None) -> nn.Module:
     """models/__init__.py:17-49: 'cnn' | 'cnn_residual' | 'cnn_large'."""
+    from . import exact_fp32_convs
+    exact_fp32_convs()  # before the model's first (fp32, MIOpen) convolution
     cfg = dict(model_cfg or {})
     in_ch = obs_shape[0]
     if name == "cnn":

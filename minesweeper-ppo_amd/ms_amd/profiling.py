@@ -78,7 +78,9 @@ class RolloutTimings(Mapping):
     """The reference's ``timings`` dict of collect_rollout (train_rl.py:278-288): steps and, per
     bucket (tensor_bridge, mine_label_copy, env_step, model_forward), ``<bucket>_total_s`` and
     ``<bucket>_per_step_ms``, measured on the GPU by a PhaseTimer and resolved on first read;
-    plus ``enqueue_total_s``, the host time the loop took to enqueue.
+    plus ``enqueue_total_s``, the host time the loop took to enqueue. With timing disabled
+    (``collect_rollout(timing=False)``) no events exist and only ``steps`` and
+    ``enqueue_total_s`` are present. ``to_dict()`` gives a plain dict (json-serialisable).
 
     On this path the buckets mean: tensor_bridge = the device-side hand-offs that replace the
     reference's PCIe copies (obs -> cell codes, values -> buffer), mine_label_copy = ms_labels,
@@ -94,7 +96,7 @@ class RolloutTimings(Mapping):
         if self._d is None:
             tot = self._timer.totals()
             d: Dict[str, float] = {"steps": self._steps}
-            for b in self.BUCKETS:
+            for b in (self.BUCKETS if self._timer.enabled else ()):
                 s = tot.get(b, 0.0)
                 d[f"{b}_total_s"] = s
                 d[f"{b}_per_step_ms"] = (s / self._steps) * 1000.0 if self._steps else 0.0
@@ -113,6 +115,9 @@ class RolloutTimings(Mapping):
 
     def __repr__(self) -> str:
         return repr(self._resolve())
+
+    def to_dict(self) -> Dict[str, float]:
+        return dict(self._resolve())
 
 
 __all__ = ["prange", "PhaseTimer", "RolloutTimings"]

@@ -61,10 +61,22 @@ struct TFLayer {
   uint8_t* rmask;       // [N][P][12] ReLU bits or NULL
 };
 
+#ifdef MC_DIAG
+#define TSTAMP(k)                                               \
+  do {                                                          \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    dacc[k] += t_ - tlast;                                      \
+    tlast = t_;                                                 \
+  } while (0)
+#else
+#define TSTAMP(k) do { } while (0)
+#endif
+
 template <typename E>
 struct TrunkFwdParams {
   const E* x0;  // [N][P][96] block 0's input
   E* ws;        // [grid][P][96]: block outputs that are not kept (residual of the next block)
+  unsigned long long* diag;  // MC_DIAG builds: per-wave phase cycle totals [grid][4][8]
   int NL, N, H, W;
   float eps;
   TFLayer<E> L[MAXL];
@@ -126,6 +138,10 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_fwd(TrunkFwdPar
     qc[t] = q < P ? q - qr[t] * W : -1000;
   }
   u32x4 wr[NWC];
+#ifdef MC_DIAG
+  unsigned long long dacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tlast = __builtin_amdgcn_s_memtime();
+#endif
 
   for (int n = blockIdx.x; n < p.N; n += gridDim.x) {
     const size_t so = (size_t)n * P * COUT;  // this sample's offset in every [N][P][96] tensor
@@ -171,6 +187,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_fwd(TrunkFwdPar
 #pragma unroll
           for (int i = 0; i < 16; ++i) acc[t][ct][i] = 0.f;
 
+      TSTAMP(0);
       for (int tap = 0; tap < 9; ++tap) {
         if (tap + 1 < 9) load_wtap<E, NWC>(wt, tap + 1, tid, wr);
         const int dr = tap / 3 - 1, dc = tap % 3 - 1;
@@ -211,6 +228,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_fwd(TrunkFwdPar
           __syncthreads();
         }
       }
+      TSTAMP(1);
       // the next layer's tap-0 weights: loaded now, written to sW (free) after the statistics
       const bool more = l + 1 < p.NL;
       if (more) load_wtap<E, NWC>(p.L[l + 1].wt, 0, tid, wr);
@@ -261,6 +279,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_fwd(TrunkFwdPar
         }
         __syncthreads();  // sRed reused by the next pass
       }
+      TSTAMP(2);
       float* stats = p.L[l].stats;
       if (stats && tid < NGRP) {
         float m = 0.f, r = 0.f;
@@ -300,6 +319,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_fwd(TrunkFwdPar
         sAB[2 * COUT + tid] = dmask ? dmask[(size_t)n * COUT + tid] : 1.0f;
       }
       __syncthreads();
+      TSTAMP(3);
 
       // ---------------- epilogue: 16-B chunks of [px][co], written in place ----------------
       // residual (conv2 of block b): the block input = block 0's input, or block b-1's output
@@ -360,8 +380,13 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_fwd(TrunkFwdPar
         }
       }
       __syncthreads();  // the tile and sAB are complete / free
+      TSTAMP(4);
     }
   }
+#ifdef MC_DIAG
+  if (p.diag && (threadIdx.x & 63) == 0)
+    for (int k = 0; k < 8; ++k) p.diag[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + k] = dacc[k];
+#endif
 }
 
 // ------------------------------------------------------------------------------------
@@ -381,6 +406,7 @@ struct TrunkBwdParams {
   const E* dout;  // [N][P][96] gradient of the last layer's output
   E* ws;          // [grid][P][96]: a block's skip gradient between its conv2 and its input
   float* part;    // [VG][NL][3][96] d gamma, d beta, d bias per partial row
+  unsigned long long* diag;  // MC_DIAG builds: per-wave phase cycle totals [grid][4][8]
   int NL, N, H, W;
   int VG;         // partial rows: the per-layer kernel's grid (min(N, 2 x CUs)), so the sums match it
   TBLayer<E> L[MAXL + 1];
@@ -425,6 +451,10 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_bwd(TrunkBwdPar
     qc[t] = q < P ? q - qr[t] * W : -1000;
   }
   constexpr int NWC = (COUT * C8 + 255) / 256;  // 16-B chunks of one W^T tap per thread
+#ifdef MC_DIAG
+  unsigned long long dacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tlast = __builtin_amdgcn_s_memtime();
+#endif
 
   // partial row vb takes samples vb, vb + VG, ... in order, as workgroup vb of the per-layer
   // kernel does; a workgroup runs rows blockIdx.x, blockIdx.x + gridDim.x, ... (VG >= gridDim.x)
@@ -525,6 +555,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_bwd(TrunkBwdPar
           }
         }
       }
+      TSTAMP(0);
       // tap 0's W^T: loaded here, its latency hidden behind the channel reductions
       const E* wT = p.L[li].wT;
       const bool dgrad = li > 0;
@@ -580,6 +611,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_bwd(TrunkBwdPar
       }
       __syncthreads();
 
+      TSTAMP(1);
       // tap 0's W^T goes to sW (free now: the sums are read) before pass 2 issues its stores
       if (dgrad) {
 #pragma unroll
@@ -616,8 +648,12 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_bwd(TrunkBwdPar
           }
         }
       }
-      if (!dgrad) continue;  // (uniform) the stem's input needs no gradient
+      if (!dgrad) {  // (uniform) the stem's input needs no gradient
+        TSTAMP(2);
+        continue;
+      }
       __syncthreads();
+      TSTAMP(2);
 
       // ---------------- dgrad: dx = sum_tap shift(dy) . W^T[tap] ----------------
       f32x16 acc[NPT][3];
@@ -686,6 +722,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_bwd(TrunkBwdPar
           __syncthreads();
         }
       }
+      TSTAMP(3);
       // dx -> the tile (16-bit, as the per-layer kernel's dx store): layer li-1's dout
 #pragma unroll
       for (int t = 0; t < NPT; ++t)
@@ -697,8 +734,13 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_bwd(TrunkBwdPar
             if (px < P) sD[px * DCP + ct * 32 + l32] = (E)acc[t][ct][i];
           }
       __syncthreads();
+      TSTAMP(4);
     }
   }
+#ifdef MC_DIAG
+  if (p.diag && (threadIdx.x & 63) == 0)
+    for (int k = 0; k < 8; ++k) p.diag[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + k] = dacc[k];
+#endif
 }
 
 // out[i] = sum_g part[g * n + i] in fixed order (k_reduce of mscnn_bwd.hip, small n)
@@ -753,6 +795,10 @@ int launched(const char* what) {
   return MS_OK;
 }
 
+#ifdef MC_DIAG
+unsigned long long* g_trunk_diag[2] = {nullptr, nullptr};
+#endif
+
 template <typename E, int NPT, bool FULL>
 int launch_trunk_fwd(const TrunkFwdParams<E>& p, hipStream_t s) {
   static bool attr = false;
@@ -774,6 +820,9 @@ int run_trunk_fwd(const uint16_t* x0, const mc_fwd_layer* layers, int nl, void* 
   p.H = h;
   p.W = w;
   p.eps = eps;
+#ifdef MC_DIAG
+  p.diag = g_trunk_diag[0];
+#endif
   for (int l = 0; l < nl; ++l) {
     const mc_fwd_layer& a = layers[l];
     p.L[l].wt = reinterpret_cast<const E*>(a.w);
@@ -816,6 +865,9 @@ int run_trunk_bwd(const uint16_t* dout, const mc_bwd_layer* layers, int nl, floa
   p.ws = reinterpret_cast<E*>(work);
   p.part = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(work) + (size_t)grid * P * COUT * 2);
   p.VG = trunk_vgrid(n);
+#ifdef MC_DIAG
+  p.diag = g_trunk_diag[1];
+#endif
   p.NL = nl;
   p.N = n;
   p.H = h;
@@ -856,6 +908,14 @@ bool trunk_shape_ok(int n, int h, int w, int nl, int max_nl, const char* what) {
 }  // namespace
 
 extern "C" {
+
+#ifdef MC_DIAG
+// diagnostics only (not in mscnn.h): per-wave phase cycle totals of the next trunk launches
+void mc_set_trunk_diag(unsigned long long* fwd, unsigned long long* bwd) {
+  g_trunk_diag[0] = fwd;
+  g_trunk_diag[1] = bwd;
+}
+#endif
 
 int64_t mc_trunk_fwd_workspace(int32_t n, int32_t h, int32_t w_) {
   if (n <= 0 || h <= 0 || w_ <= 0 || h * w_ > 512) return -1;

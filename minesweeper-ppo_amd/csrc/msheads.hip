@@ -11,15 +11,14 @@
 //   rows from LDS, B = f rows loaded straight from HBM), bias + ReLU + the w2 dot
 //   product in registers (the channel sum is in-lane plus one lane^32 add), one f32
 //   logit per row and head. f is read once for both heads; h never reaches HBM.
-// k_heads_bwd: per 64-row tile (two workgroups per CU: 78.8 KB of LDS each), recompute
-//   H[px][c] (A = f tile in LDS, B = W1),
-//   dh = dlogit * w2 * (h > 0) written to an LDS image (bf16), then
+// k_heads_bwd: one workgroup per CU streams 64-row f tiles through an LDS-DMA ring (below);
+//   per tile it recomputes H, writes dh = dlogit * w2 * (h > 0) to an LDS image, then
 //     df^T = W1p^T . dh_p^T  (policy only: the mine head sees f.detach(); W1p^T read from
 //                             the W1 image with ds_read_b64_tr_b16),
 //     dW1 += dh^T . f        (K = the tile's pixels; both operands K-major via
 //                             ds_read_b64_tr_b16 from the LDS images),
 //     dw2 += h^T . dlogit, db1 += sum dh  (in-lane accumulators);
-//   per-workgroup partials are summed by k_heads_reduce.
+//   per-workgroup partials are summed by k_heads_reduce in fixed order (deterministic).
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -133,7 +132,6 @@ struct HeadBwdParams {
   const float* dlp;
   const float* dlm;
   const E* w1;   // [192][96]
-  const E* w1pT; // unused (round 2's policy W1^T copy)
   const float* b1;
   const float* w2;
   const float* gadd;  // [M / P][96] or null: added to df (the value head's pooled gradient / P)
@@ -141,130 +139,221 @@ struct HeadBwdParams {
   float* part;        // [gridDim][PART]
   int64_t M;
   int P;
-  int exp;            // MC_WSX builds: timing experiments (HBX_* bits; results wrong)
+  unsigned long long* diag;  // MC_DIAG builds: per-wave phase cycle totals [grid][4 waves][8]
 };
-// timing experiments of k_heads_bwd (libmsenv_wsx.so, mc_set_heads_exp; tools/heads_bwd_exp.py):
-// each bit removes one part so its cost can be read off the launch time
-#ifdef MC_WSX
-#define HBX(bit) ((p.exp & (bit)) != 0)
-#else
-#define HBX(bit) false
-#endif
-[[maybe_unused]] constexpr int HBX_NO_DF_STORE = 1, HBX_NO_DW1 = 2, HBX_NO_H = 4, HBX_NO_FLOAD = 8,
-                               HBX_NO_DH_WRITE = 16, HBX_NO_DF = 32;
 
-// f tile [128][96]: 16-B chunk ch of row r at chunk ch ^ ((r >> 2) & 3)
+#ifdef MC_DIAG
+#define HSTAMP(k)                                               \
+  do {                                                          \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    dacc[k] += t_ - tlast;                                      \
+    tlast = t_;                                                 \
+  } while (0)
+#else
+#define HSTAMP(k) do { } while (0)
+#endif
+
+// f tile [64][96]: 16-B chunk ch of row r at chunk ch ^ ((r >> 2) & 3)
 __device__ __forceinline__ int sf_off(int r, int col) {
   return r * C + 8 * ((col >> 3) ^ ((r >> 2) & 3)) + (col & 7);
 }
-// dh image [128][192]: chunk ch of row r at ch ^ (((r >> 1) & 1) << 2 | (r >> 2) & 3)
+// dh image [64][192]: chunk ch of row r at ch ^ (((r >> 1) & 1) << 2 | (r >> 2) & 3)
 __device__ __forceinline__ int sd_off(int r, int col) {
   return r * NH + 8 * ((col >> 3) ^ ((((r >> 1) & 1) << 2) | ((r >> 2) & 3))) + (col & 7);
 }
 
-// k_heads_bwd LDS (78.8 KB: two workgroups per CU). 64-row tiles; the policy W1^T operand
-// of df is read from the W1 image by transposing LDS reads, so no W1^T copy is kept.
-constexpr int TRB = 64;  // rows per backward tile
+// k_heads_bwd: one 256-thread workgroup per CU streams 64-row tiles through an NS-slot LDS ring
+// filled by LDS-DMA (global_load_lds: no VGPRs), so NS - 1 tiles (~58 KB) are in flight per CU
+// while the current one is computed; round 3/4's form (two workgroups per CU, each staging its
+// next tile through registers only after the current one) had at most 24 KB in flight per CU and
+// ran its staging alone at 1.1 TB/s (profiles/r04/heads_bwd_exp.txt). Per tile, wave w =
+// (px-tile pt = w & 1, head hd = w >> 1):
+//   H^T[c][px] = W1[c] . f[px] for its head's 96 channels and px-tile (A = W1 rows, B = f rows),
+//   dh = dlogit * w2 * (h > 0) -> LDS image (8-B writes: four channels of a pixel per lane),
+//   dw2 += h . dlogit, db1 += dh in-lane (lane = pixel, reduced over lanes once at the end);
+//   df^T[k][px] = sum_c W1p[c][k] dh[px][c] (policy channels only: the mine head reads f.detach())
+//     for k-tiles {0, 1} (w < 2) or {2} (w >= 2), staged in LDS and stored as 16-B rows;
+//   dW1[c][k] += sum_px dh[px][c] f[px][k] for dW1 tiles 4 / 4 / 5 / 5 of the 18 (6 c x 3 k):
+//   46 / 46 / 44 / 44 MFMAs per wave and tile.
+// Ring protocol: at the top of local iteration i each wave issues its 4 DMA instructions of tile
+// i + NS - 1 into the slot tile i - 1 left, then waits (counted vmcnt) for its own DMAs of tile i
+// and meets the others (lds_barrier): every wave's share of tile i has landed. Per iteration a
+// wave issues exactly D = 4 DMAs and S = 3 df stores, so after tile i's DMAs it has issued
+// (NS - 1) D + min(i, NS - 1) S more vector-memory instructions; near the end (fewer DMAs) it waits
+// for all. The DMAs are inline asm so the compiler does not make LDS reads wait for them.
+constexpr int TRB = 64;          // rows per tile
+constexpr int NS = 5;            // ring slots
+constexpr int DFP = 132;         // df staging row (elements; 66 dwords: conflict-free 8-B writes)
+constexpr int GA_FLOATS = 512;   // gadd rows of a tile: samples n0 .. n0 + 4 (P >= 16)
+constexpr int HB_D = 4, HB_S = 3;  // DMAs and df stores per wave and tile
+template <typename E>
+struct HeadSlot {
+  E f[TRB * C];
+  float dl[2][TRB];
+  float ga[GA_FLOATS];
+};
 template <typename E>
 struct HeadLds {
+  HeadSlot<E> ring[NS];
   E w[NH * WP];     // W1 rows [c][k]
-  E f[TRB * C];     // swizzled f tile
   E dh[TRB * NH];   // swizzled dh image; after the tile loop: the dw2 / db1 combine
-  float dl[2][TRB];
+  E dfs[TRB * DFP]; // df of the tile, [px][k]
   float b1[NH], w2[NH];
 };
-static_assert(sizeof(HeadLds<__bf16>) <= 80 * 1024, "two k_heads_bwd workgroups per CU");
+static_assert(sizeof(HeadLds<__bf16>) <= 160 * 1024, "k_heads_bwd LDS");
 
-// one wave's share of a 64-row tile: H recompute for px-tile pt (wave & 1) and head hd
-// (wave >> 1: 0 policy, 1 mine), its dh columns, df for px-tile pt and k-tiles [KT0, KT0+NKT),
-// and dW1 tiles [T0, T0+NTW) of the 18 (6 c-tiles x 3 k-tiles)
-template <typename E, int T0, int NTW, int KT0, int NKT>
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)(p);
+}
+// one full-wave LDS-DMA: 16 B (x4) or 4 B (x1) a lane, lane-linear at LDS byte address m0v
+__device__ __forceinline__ void dma_x4(const void* src, uint32_t m0v) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0v) : "memory", "m0");
+}
+__device__ __forceinline__ void dma_x1(const void* src, uint32_t m0v) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(m0v) : "memory", "m0");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt(0x0F70 | (N & 15) | ((N >> 4) << 14));
+}
+template <int I>
+__device__ __forceinline__ void wait_tile(int i) {  // vmcnt of iteration i (I = min(i, NS - 1))
+  if constexpr (I + 1 < NS) {
+    if (i == I) return wait_vm<(NS - 1) * HB_D + I * HB_S>();
+    return wait_tile<I + 1>(i);
+  } else {
+    wait_vm<(NS - 1) * (HB_D + HB_S)>();
+  }
+}
+
+// wave WV's four DMAs of global tile t into ring slot s: f chunks 3 WV .. 3 WV + 2 (LDS order,
+// so the source chunk carries the swizzle), plus dlp (wave 0), dlm (wave 1), gadd (waves 2, 3;
+// samples n0 .. n0 + 4 of the tile's rows, clamped to the buffer); without dlm / gadd a wave
+// re-loads a valid address into the unused space so that every wave issues four
+template <typename E, int WV, bool GDMA>
+__device__ __forceinline__ void heads_issue(const HeadBwdParams<E>& p, HeadSlot<E>& S, int64_t t, int lane) {
+  const int64_t base = t * TRB, last = p.M - 1;
+  const uint32_t fb = lds_addr(S.f);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int lc = (3 * WV + j) * 64 + lane, r = lc / 12, chs = lc - r * 12, ch = chs ^ ((r >> 2) & 3);
+    const int64_t row = base + r < p.M ? base + r : last;
+    dma_x4(p.f + row * C + ch * 8, fb + (3 * WV + j) * 1024);
+  }
+  const int64_t rowl = base + lane < p.M ? base + lane : last;
+  if constexpr (WV == 0) {
+    dma_x1(p.dlp + rowl, lds_addr(S.dl[0]));
+  } else if constexpr (WV == 1) {
+    dma_x1((p.dlm ? p.dlm : p.dlp) + rowl, lds_addr(S.dl[1]));
+  } else {
+    const void* src = p.f;
+    if (GDMA) {
+      const int64_t nfl = (p.M / p.P) * C;  // gadd floats
+      int64_t q = (base / p.P) * C + (WV - 2) * 256 + lane * 4;
+      q = q + 4 <= nfl ? q : nfl - 4;
+      src = p.gadd + q;
+    }
+    dma_x4(src, lds_addr(S.ga) + (WV - 2) * 1024);
+  }
+}
+
+template <typename E, int WV, bool GDMA>
 __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLds<E>& L) {
   typedef typename EV<E>::v8 E8;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hh = lane >> 5;
+  typedef typename EV<E>::v4 E4;
+  constexpr int PT = WV & 1, HD = WV >> 1;
+  constexpr int KT0 = WV < 2 ? 0 : 2, NKT = WV < 2 ? 2 : 1;  // df k-tiles
+  constexpr int T0 = WV < 2 ? 4 * WV : 8 + 5 * (WV - 2), NTW = WV < 2 ? 4 : 5;  // dW1 tiles
+  const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hh = lane >> 5;
   const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-  const int pt = wave & 1, hd = wave >> 1;
   f32x16 dwacc[NTW];
 #pragma unroll
   for (int t = 0; t < NTW; ++t)
 #pragma unroll
     for (int i = 0; i < 16; ++i) dwacc[t][i] = 0.f;
-  float dw2acc[3], db1acc[3];
+  float dw2a[3][16], db1a[3][16];  // channel (3 HD + j) * 32 + 8 (r >> 2) + 4 hh + (r & 3), this lane's pixels
 #pragma unroll
-  for (int j = 0; j < 3; ++j) dw2acc[j] = db1acc[j] = 0.f;
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dw2a[j][r] = db1a[j][r] = 0.f;
 
   const int64_t ntiles = (p.M + TRB - 1) / TRB;
-  constexpr int NFC = TRB * 12 / 256;
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int64_t base = tile * TRB;
-    const int zo = opaque0();
-    // ---- stage f tile and the two logit gradients (unconditional loads from clamped rows) ----
-    {
-      u32x4 v[NFC];
-#pragma unroll
-      for (int i = 0; i < NFC; ++i) {
-        const int c = tid + 256 * i + zo, r = c / 12, ch = c - r * 12;
-        const int64_t row = base + r < p.M ? base + r : p.M - 1;
-        v[i] = HBX(HBX_NO_FLOAD) ? u32x4{(uint32_t)c, 0u, 0u, 0u} : *reinterpret_cast<const u32x4*>(&p.f[row * C + ch * 8]);
-      }
-      const int64_t rowd = base + (tid & (TRB - 1)) < p.M ? base + (tid & (TRB - 1)) : p.M - 1;
-      const float d0 = p.dlp[rowd];
-      const float d1 = p.dlm ? p.dlm[rowd] : 0.f;
-#pragma unroll
-      for (int i = 0; i < NFC; ++i) {
-        const int c = tid + 256 * i + zo, r = c / 12, ch = c - r * 12;
-        if (base + r >= p.M) v[i] = u32x4{0u, 0u, 0u, 0u};
-        *reinterpret_cast<u32x4*>(&L.f[sf_off(r, ch * 8)]) = v[i];
-      }
-      if (tid < TRB) {
-        const bool ok = base + tid < p.M;
-        L.dl[0][tid] = ok ? d0 : 0.f;
-        L.dl[1][tid] = ok ? d1 : 0.f;
-      }
+  const int nloc = (int)((ntiles - blockIdx.x + gridDim.x - 1) / gridDim.x);  // tiles of this workgroup
+#ifdef MC_DIAG
+  unsigned long long dacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tlast = __builtin_amdgcn_s_memtime();
+#endif
+  for (int i = 0; i + 1 < NS && i < nloc; ++i) heads_issue<E, WV, GDMA>(p, L.ring[i], blockIdx.x + (int64_t)i * gridDim.x, lane);
+  const bool mine_dl = HD == 0 || p.dlm != nullptr;
+  for (int i = 0; i < nloc; ++i) {
+    const int64_t tile = blockIdx.x + (int64_t)i * gridDim.x, base = tile * TRB;
+    HSTAMP(7);
+    if (i + NS - 1 < nloc) {
+      heads_issue<E, WV, GDMA>(p, L.ring[(i + NS - 1) % NS], tile + (int64_t)(NS - 1) * gridDim.x, lane);
+      HSTAMP(0);
+      wait_tile<0>(i);
+    } else {
+      HSTAMP(0);
+      wait_vm<0>();
     }
-    __syncthreads();
-    // ---- recompute H[px][c] for px-tile pt and this head's three c-tiles; dh -> LDS ----
+    HSTAMP(1);
+    lds_barrier();  // every wave's share of tile i has landed
+    HSTAMP(2);
+    const HeadSlot<E>& S = L.ring[i % NS];
+    const int zo = opaque0();
+
+    // ---- H^T for this head's 96 channels and px-tile PT; dh -> LDS; dw2 / db1 in-lane ----
     {
       f32x16 acc[3];
 #pragma unroll
       for (int j = 0; j < 3; ++j)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
-      const int ra = pt * 32 + l32 + zo;
-#pragma unroll 1
-      for (int ks = 0; ks < (HBX(HBX_NO_H) ? 0 : 6); ++ks) {
-        const E8 a = *reinterpret_cast<const E8*>(&L.f[sf_off(ra, ks * 16 + 8 * hh)]);
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+      const int px = PT * 32 + l32;
+#pragma unroll
+      for (int ks = 0; ks < 6; ++ks) {
+        const E8 b = *reinterpret_cast<const E8*>(&S.f[sf_off(px, ks * 16 + 8 * hh) + zo]);
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-          const E8 b = *reinterpret_cast<const E8*>(&L.w[((3 * hd + j) * 32 + l32) * WP + ks * 16 + 8 * hh + zo]);
+          const E8 a = *reinterpret_cast<const E8*>(&L.w[((3 * HD + j) * 32 + l32) * WP + ks * 16 + 8 * hh + zo]);
           acc[j] = mfma32(a, b, acc[j]);
         }
       }
-      // acc[j][r] = H[px = pt*32 + 8*(r>>2) + 4*hh + (r&3)][c = (3*hd + j)*32 + l32]
+      const float dl = (base + px < p.M && mine_dl) ? S.dl[HD][px] : 0.f;
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const int c = (3 * hd + j) * 32 + l32;
-        const float b1c = L.b1[c + zo], w2c = L.w2[c + zo];
+      for (int j = 0; j < 3; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int pr = pt * 32 + 8 * (r >> 2) + 4 * hh + (r & 3) + zo;
-          const float dl = L.dl[hd][pr];
-          const float hv = fmaxf(acc[j][r] + b1c, 0.f);
-          dw2acc[j] += hv * dl;
-          const float dh = hv > 0.f ? dl * w2c : 0.f;
-          db1acc[j] += dh;
-          if (!HBX(HBX_NO_DH_WRITE)) L.dh[sd_off(pr, c)] = (E)dh;
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int c0 = (3 * HD + j) * 32 + 8 * g4 + 4 * hh;
+          const float4 bb = *reinterpret_cast<const float4*>(&L.b1[c0 + zo]);
+          const float4 ww = *reinterpret_cast<const float4*>(&L.w2[c0 + zo]);
+          const float bv[4] = {bb.x, bb.y, bb.z, bb.w}, wv[4] = {ww.x, ww.y, ww.z, ww.w};
+          E4 d4;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * g4 + e;
+            const float hv = fmaxf(acc[j][r] + bv[e], 0.f);
+            dw2a[j][r] += hv * dl;
+            const float dh = hv > 0.f ? dl * wv[e] : 0.f;
+            db1a[j][r] += dh;
+            d4[e] = (E)dh;
+          }
+          *reinterpret_cast<E4*>(&L.dh[sd_off(px, c0)]) = d4;
         }
-      }
     }
-    __syncthreads();
-    // ---- df^T[k][px] = sum_c W1p[c][k] dh[px][c] (policy channels only), px-tile pt ----
+    HSTAMP(3);
+    lds_barrier();
+    HSTAMP(2);
+    // ---- df^T[k][px] = sum_c W1p[c][k] dh[px][c], k-tiles KT0 .., px-tile PT -> dfs ----
     {
+      const int rb = PT * 32 + l32;
       f32x16 acc2[NKT];
-      const int rb = pt * 32 + l32 + zo;
-      const int64_t row = base + rb;
-      if (p.gadd) {  // (uniform) the accumulators start at gadd[m / P] (rows past M: row M-1, discarded)
-        const float* ga = p.gadd + ((row < p.M ? row : p.M - 1) / p.P) * C;
+      if (p.gadd) {  // (uniform) the accumulators start at gadd[row / P]
+        const int64_t rowc = base + rb < p.M ? base + rb : p.M - 1;
+        const float* ga;
+        if constexpr (GDMA) ga = S.ga + (rowc / p.P - base / p.P) * C;
+        else ga = p.gadd + (rowc / p.P) * C;
 #pragma unroll
         for (int u = 0; u < NKT; ++u)
 #pragma unroll
@@ -279,11 +368,11 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
 #pragma unroll
         for (int u = 0; u < NKT; ++u)
 #pragma unroll
-          for (int i = 0; i < 16; ++i) acc2[u][i] = 0.f;
+          for (int r = 0; r < 16; ++r) acc2[u][r] = 0.f;
       }
-#pragma unroll 1
-      for (int ks = 0; ks < (HBX(HBX_NO_DF) ? 0 : 6); ++ks) {
-        const E8 b = *reinterpret_cast<const E8*>(&L.dh[sd_off(rb, ks * 16 + 8 * hh)]);
+#pragma unroll
+      for (int ks = 0; ks < 6; ++ks) {
+        const E8 b = *reinterpret_cast<const E8*>(&L.dh[sd_off(rb, ks * 16 + 8 * hh) + zo]);
         const int r0 = ks * 16 + 8 * (g >> 1) + q + zo;  // W1 rows (K = c), transposed read
 #pragma unroll
         for (int u = 0; u < NKT; ++u) {
@@ -292,24 +381,18 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
           acc2[u] = mfma32(a, b, acc2[u]);
         }
       }
-      // acc2[u][r] = df[px = rb][k = (KT0+u)*32 + 8*(r>>2) + 4*hh + (r&3)]: 8-B stores (staging
-      // them in LDS for 16-B stores needs the f region, i.e. dW1 first: 3.26 ms, spills)
-      if (row < p.M && !HBX(HBX_NO_DF_STORE)) {
-        typedef typename EV<E>::v4 E4;
+      // acc2[u][r] = df[px = rb][k = (KT0 + u) * 32 + 8 (r >> 2) + 4 hh + (r & 3)]
 #pragma unroll
-        for (int u = 0; u < NKT; ++u)
+      for (int u = 0; u < NKT; ++u)
 #pragma unroll
-          for (int gg = 0; gg < 4; ++gg) {
-            const int k0 = (KT0 + u) * 32 + 8 * gg + 4 * hh;
-            *reinterpret_cast<E4*>(&p.df[row * C + k0]) =
-                E4{(E)acc2[u][4 * gg + 0], (E)acc2[u][4 * gg + 1], (E)acc2[u][4 * gg + 2], (E)acc2[u][4 * gg + 3]};
-          }
-      }
+        for (int gg = 0; gg < 4; ++gg)
+          *reinterpret_cast<E4*>(&L.dfs[rb * DFP + (KT0 + u) * 32 + 8 * gg + 4 * hh]) =
+              E4{(E)acc2[u][4 * gg + 0], (E)acc2[u][4 * gg + 1], (E)acc2[u][4 * gg + 2], (E)acc2[u][4 * gg + 3]};
     }
-
+    HSTAMP(4);
     // ---- dW1[c][k] += sum_px dh[px][c] f[px][k] over the tile's 64 rows ----
-#pragma unroll 1
-    for (int kk = 0; kk < (HBX(HBX_NO_DW1) ? 0 : TRB / 16); ++kk) {
+#pragma unroll
+    for (int kk = 0; kk < TRB / 16; ++kk) {
       const int r0 = kk * 16 + 8 * (g >> 1) + q + zo;
       E8 av[6], bv[3];
 #pragma unroll
@@ -320,7 +403,7 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
 #pragma unroll
       for (int kt = 0; kt < 3; ++kt) {
         const int col = kt * 32 + 16 * (g & 1) + 4 * pp;
-        bv[kt] = cat8(lds_tr4(&L.f[sf_off(r0, col)]), lds_tr4(&L.f[sf_off(r0 + 4, col)]));
+        bv[kt] = cat8(lds_tr4(&S.f[sf_off(r0, col)]), lds_tr4(&S.f[sf_off(r0 + 4, col)]));
       }
 #pragma unroll
       for (int t = 0; t < NTW; ++t) {
@@ -328,9 +411,23 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
         dwacc[t] = mfma32(av[tt / 3], bv[tt % 3], dwacc[t]);
       }
     }
-    __syncthreads();  // f / dh images are re-staged by the next tile
+    HSTAMP(5);
+    lds_barrier();  // dfs complete; the slot, dh and dfs are free after the stores' reads below
+    HSTAMP(2);
+    // ---- df rows: 16-B chunks, whole 192-B rows (exactly HB_S stores a wave on a full tile) ----
+#pragma unroll
+    for (int k = 0; k < HB_S; ++k) {
+      const int c = tid + 256 * k, r = c / 12, ch = c - r * 12;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(&L.dfs[r * DFP + ch * 8]);
+      if (base + r < p.M) *reinterpret_cast<u32x4*>(&p.df[(base + r) * C + ch * 8]) = v;
+    }
   }
-  // ---- partials ----
+#ifdef MC_DIAG
+  if (p.diag && lane == 0)
+    for (int k = 0; k < 8; ++k) p.diag[((size_t)blockIdx.x * 4 + WV) * 8 + k] = dacc[k];
+#endif
+  // ---- partials: dW1 tiles; dw2 / db1 summed over the lanes (pixels), the two px-tile waves
+  // of a head combined in fixed order by the caller (LDS: the dh region) ----
   float* part = p.part + (size_t)blockIdx.x * PART;
 #pragma unroll
   for (int t = 0; t < NTW; ++t) {
@@ -341,20 +438,31 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
       part[c * C + kt * 32 + l32] = dwacc[t][r];
     }
   }
-  // dw2 / db1: the two waves of a head (px-tiles 0 and 1) combine in LDS (the dh region,
-  // free after the tile loop's last barrier)
-  float* red = reinterpret_cast<float*>(L.dh);  // [2][NH]
-  for (int i = tid; i < 2 * NH; i += 256) red[i] = 0.f;
-  __syncthreads();
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    atomicAdd(&red[(3 * hd + j) * 32 + l32], dw2acc[j]);
-    atomicAdd(&red[NH + (3 * hd + j) * 32 + l32], db1acc[j]);
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) {
+        dw2a[j][r] += __shfl_xor(dw2a[j][r], o);
+        db1a[j][r] += __shfl_xor(db1a[j][r], o);
+      }
+  lds_barrier();  // the dh region is free
+  float* red = reinterpret_cast<float*>(L.dh);  // [2 pt][2][NH]
+  if (l32 == 0) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int c = (3 * HD + j) * 32 + 8 * (r >> 2) + 4 * hh + (r & 3);
+        red[(PT * 2 + 0) * NH + c] = dw2a[j][r];
+        red[(PT * 2 + 1) * NH + c] = db1a[j][r];
+      }
   }
 }
 
-template <typename E>
-__global__ __launch_bounds__(256, 2) void k_heads_bwd(HeadBwdParams<E> p) {
+template <typename E, bool GDMA>
+__global__ __launch_bounds__(256, 1) void k_heads_bwd(HeadBwdParams<E> p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   HeadLds<E>& L = *reinterpret_cast<HeadLds<E>*>(smem);
   const int tid = threadIdx.x;
@@ -366,21 +474,20 @@ __global__ __launch_bounds__(256, 2) void k_heads_bwd(HeadBwdParams<E> p) {
     L.b1[i] = p.b1[i];
     L.w2[i] = p.w2[i];
   }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the staging loads are done before the DMAs start
   __syncthreads();
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // 18 dW1 tiles split 5/5/4/4; the 6 df tiles (2 px x 3 k) split 2/2/1/1
-  switch (wave) {
-    case 0: heads_bwd_body<E, 0, 5, 0, 2>(p, L); break;
-    case 1: heads_bwd_body<E, 5, 5, 0, 2>(p, L); break;
-    case 2: heads_bwd_body<E, 10, 4, 2, 1>(p, L); break;
-    default: heads_bwd_body<E, 14, 4, 2, 1>(p, L); break;
+  switch (__builtin_amdgcn_readfirstlane(tid >> 6)) {
+    case 0: heads_bwd_body<E, 0, GDMA>(p, L); break;
+    case 1: heads_bwd_body<E, 1, GDMA>(p, L); break;
+    case 2: heads_bwd_body<E, 2, GDMA>(p, L); break;
+    default: heads_bwd_body<E, 3, GDMA>(p, L); break;
   }
   __syncthreads();
-  const float* red = reinterpret_cast<const float*>(L.dh);  // the dw2 / db1 combine of the bodies
+  const float* red = reinterpret_cast<const float*>(L.dh);
   float* part = p.part + (size_t)blockIdx.x * PART;
   for (int i = tid; i < NH; i += 256) {
-    part[NH * C + i] = red[i];
-    part[NH * C + NH + i] = red[NH + i];
+    part[NH * C + i] = red[0 * NH + i] + red[2 * NH + i];
+    part[NH * C + NH + i] = red[1 * NH + i] + red[3 * NH + i];
   }
 }
 
@@ -417,9 +524,9 @@ __global__ __launch_bounds__(256) void k_heads_reduce(const float* __restrict__ 
   }
 }
 
-int bwd_grid(int64_t M) {  // two k_heads_bwd workgroups per CU
+int bwd_grid(int64_t M) {  // one k_heads_bwd workgroup per CU
   const int64_t ntiles = (M + TRB - 1) / TRB;
-  const int cap = 2 * num_cus();
+  const int cap = num_cus();
   return (int)(ntiles < cap ? ntiles : cap);
 }
 
@@ -452,20 +559,31 @@ int run_heads_fwd(const uint16_t* f, const uint16_t* w1, const float* b1, const 
   return check("k_heads_fwd");
 }
 
-#ifdef MC_WSX
-int g_heads_exp = 0;
+#ifdef MC_DIAG
+unsigned long long* g_heads_diag = nullptr;
 #endif
 
+template <typename E, bool GDMA>
+int launch_heads_bwd(const HeadBwdParams<E>& p, int grid, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_heads_bwd<E, GDMA>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)sizeof(HeadLds<E>));
+    attr = true;
+  }
+  hipLaunchKernelGGL((k_heads_bwd<E, GDMA>), dim3(grid), dim3(256), sizeof(HeadLds<E>), s, p);
+  return check("k_heads_bwd");
+}
+
 template <typename E>
-int run_heads_bwd(const uint16_t* f, const float* dlp, const float* dlm, const uint16_t* w1, const uint16_t* w1pT,
-                  const float* b1, const float* w2, const float* gadd, int32_t P, uint16_t* df, float* dw1, float* db1,
-                  float* dw2, float* work, int64_t M, int grid, hipStream_t s) {
+int run_heads_bwd(const uint16_t* f, const float* dlp, const float* dlm, const uint16_t* w1, const float* b1,
+                  const float* w2, const float* gadd, int32_t P, uint16_t* df, float* dw1, float* db1, float* dw2,
+                  float* work, int64_t M, int grid, hipStream_t s) {
   HeadBwdParams<E> p;
   p.f = reinterpret_cast<const E*>(f);
   p.dlp = dlp;
   p.dlm = dlm;
   p.w1 = reinterpret_cast<const E*>(w1);
-  p.w1pT = reinterpret_cast<const E*>(w1pT);
   p.b1 = b1;
   p.w2 = w2;
   p.gadd = gadd;
@@ -473,18 +591,13 @@ int run_heads_bwd(const uint16_t* f, const float* dlp, const float* dlm, const u
   p.part = work;
   p.M = M;
   p.P = P;
-  p.exp = 0;
-#ifdef MC_WSX
-  p.exp = g_heads_exp;
+  p.diag = nullptr;
+#ifdef MC_DIAG
+  p.diag = g_heads_diag;
 #endif
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_heads_bwd<E>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)sizeof(HeadLds<E>));
-    attr = true;
-  }
-  hipLaunchKernelGGL(k_heads_bwd<E>, dim3(grid), dim3(256), sizeof(HeadLds<E>), s, p);
-  int rc = check("k_heads_bwd");
+  // gadd rows by LDS-DMA need a tile to span at most 5 samples (P >= 16); smaller boards read
+  // them with plain loads (correct, slower: the compiler's waits for them also wait for the ring)
+  const int rc = (gadd && P < 16) ? launch_heads_bwd<E, false>(p, grid, s) : launch_heads_bwd<E, true>(p, grid, s);
   if (rc) return rc;
   hipLaunchKernelGGL(k_heads_reduce, dim3((PART + HR_IB - 1) / HR_IB), dim3(256), 0, s, (const float*)work, grid, dw1,
                      dw2, db1);
@@ -495,9 +608,9 @@ int run_heads_bwd(const uint16_t* f, const float* dlp, const float* dlm, const u
 
 extern "C" {
 
-#ifdef MC_WSX
-// timing experiments only (tools/heads_bwd_exp.py): HBX_* bits of the next k_heads_bwd launches
-void mc_set_heads_exp(int32_t e) { g_heads_exp = e; }
+#ifdef MC_DIAG
+// diagnostics only (not in mscnn.h): per-wave phase cycle totals of the next heads backwards
+void mc_set_heads_diag(unsigned long long* d) { g_heads_diag = d; }
 #endif
 
 int mc_heads_fwd(const uint16_t* f, const uint16_t* w1, const float* b1, const float* w2, const float* b2,
@@ -532,9 +645,9 @@ int mc_heads_bwd(const uint16_t* f, const float* dlp, const float* dlm, const ui
     return MS_EINVAL;
   }
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == MC_DT_BF16) return run_heads_bwd<__bf16>(f, dlp, dlm, w1, w1pT, b1, w2, gadd, P, df, dw1, db1, dw2, work, M, grid, s);
+  if (dtype == MC_DT_BF16) return run_heads_bwd<__bf16>(f, dlp, dlm, w1, b1, w2, gadd, P, df, dw1, db1, dw2, work, M, grid, s);
   if (dtype == MC_DT_F16)
-    return run_heads_bwd<_Float16>(f, dlp, dlm, w1, w1pT, b1, w2, gadd, P, df, dw1, db1, dw2, work, M, grid, s);
+    return run_heads_bwd<_Float16>(f, dlp, dlm, w1, b1, w2, gadd, P, df, dw1, db1, dw2, work, M, grid, s);
   snprintf(g_err, sizeof g_err, "mc_heads_bwd: dtype %d unsupported (0 bf16, 1 f16)", dtype);
   return MS_EINVAL;
 }

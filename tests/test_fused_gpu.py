@@ -184,7 +184,7 @@ def test_conv_gn_bwd_matches_torch(gpu, H, W, cin, n, with_res, dt):
         assert _rel(dx, nhwc(xq.grad) + (add.float() if add is not None else 0)) < 6e-2
 
 
-@pytest.mark.parametrize("n,P", [(300, 256), (7, 81), (3, 30), pytest.param(32768, 256, id="c2-32768x256"),
+@pytest.mark.parametrize("n,P", [(300, 256), (7, 81), (3, 30), (50, 12), pytest.param(32768, 256, id="c2-32768x256"),
                                  pytest.param(65536, 81, id="c3-65536x81"), pytest.param(8192, 480, id="c5-8192x480")])
 @pytest.mark.parametrize("with_mine", [True, False])
 @pytest.mark.parametrize("dt", DT)
@@ -226,3 +226,27 @@ def test_heads_match_torch(gpu, n, P, with_mine, dt):
     ref.update({"m" + k: v.grad for k, v in mine.named_parameters()} if with_mine else {})
     for k in ref:
         assert _rel(got[k], ref[k]) < 1e-2, (k, _rel(got[k], ref[k]))
+
+
+@pytest.mark.parametrize("n,P", [(2048, 256), (1000, 81), (9, 12)])
+def test_heads_bwd_deterministic(gpu, n, P):
+    """Two backward passes of the heads on the same inputs give bitwise-equal gradients (the
+    per-workgroup partials are combined in a fixed order; round 4's LDS float atomics for dw2 /
+    db1 were not, and the RCCL world-1 check caught it)."""
+    from ms_amd.fused import heads_apply
+    torch.manual_seed(5)
+    mk = lambda: torch.nn.Sequential(torch.nn.Conv2d(96, 96, 1), torch.nn.ReLU(),  # noqa: E731
+                                     torch.nn.Conv2d(96, 1, 1)).to(gpu)
+    pol, mine = mk(), mk()
+    f0 = (torch.randn(n, P, 96, device=gpu) * 0.7).to(torch.float16)
+    wl, wp, wm = torch.randn(n, P, device=gpu), torch.randn(n, 96, device=gpu), torch.randn(n, P, device=gpu)
+    outs = []
+    for _ in range(2):
+        for mod in (pol, mine):
+            mod.zero_grad(set_to_none=True)
+        f = f0.clone().requires_grad_(True)
+        lp, pooled, lm = heads_apply(f, pol, mine)
+        ((lp * wl).sum() + (pooled * wp).sum() + (lm * wm).sum()).backward()
+        outs.append([f.grad.clone()] + [p.grad.clone() for p in list(pol.parameters()) + list(mine.parameters())])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

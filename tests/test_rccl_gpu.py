@@ -64,7 +64,14 @@ def run(group):
 
 g0, p0, s0, _ = run(None)
 g1, p1, s1, fg = run(dist.group.WORLD)
+g2, p2, s2, _ = run(None)
+
+def diff(a, b):
+    d = (a - b).abs()
+    return {"n": int((d > 0).sum()), "max": float(d.max()), "first": int((d > 0).nonzero()[0]) if (d > 0).any() else -1}
+
 res = {"grads_equal": bool(torch.equal(g0, g1)), "params_equal": bool(torch.equal(p0, p1)),
+       "repeat_equal": bool(torch.equal(g0, g2)), "diff_group": diff(g0, g1), "diff_repeat": diff(g0, g2),
        "loss": [float(s0["loss"]), float(s1["loss"])], "finite": bool(torch.isfinite(g1).all()),
        "flat_numel": fg.flat.numel()}
 for _ in range(5):

@@ -196,21 +196,30 @@ template <typename E>
 struct HeadLds {
   HeadSlot<E> ring[NS];
   E w[NH * WP];     // W1 rows [c][k]
-  E dh[TRB * NH];   // swizzled dh image; after the tile loop: the dw2 / db1 combine
+  E dh[TRB * NH];   // swizzled dh image; after the tile loop: the dw2 combine
   E dfs[TRB * DFP]; // df of the tile, [px][k]
-  float b1[NH], w2[NH];
+  f32x4 w2v[NH / 4];
 };
 static_assert(sizeof(HeadLds<__bf16>) <= 160 * 1024, "k_heads_bwd LDS");
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)(p);
 }
-// one full-wave LDS-DMA: 16 B (x4) or 4 B (x1) a lane, lane-linear at LDS byte address m0v
+// one full-wave LDS-DMA: 16 B (x4) or 4 B (x1) a lane, lane-linear at LDS byte address m0v;
+// from a 64-bit per-lane address, or (_s) a wave-uniform base plus a 32-bit per-lane offset
 __device__ __forceinline__ void dma_x4(const void* src, uint32_t m0v) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0v) : "memory", "m0");
 }
 __device__ __forceinline__ void dma_x1(const void* src, uint32_t m0v) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(m0v) : "memory", "m0");
+}
+__device__ __forceinline__ void dma_x4_s(const void* base, uint32_t off, uint32_t m0v) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(base), "s"(m0v)
+               : "memory", "m0");
+}
+__device__ __forceinline__ void dma_x1_s(const void* base, uint32_t off, uint32_t m0v) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1" ::"v"(off), "s"(base), "s"(m0v)
+               : "memory", "m0");
 }
 template <int N>
 __device__ __forceinline__ void wait_vm() {
@@ -230,31 +239,44 @@ __device__ __forceinline__ void wait_tile(int i) {  // vmcnt of iteration i (I =
 // wave WV's four DMAs of global tile t into ring slot s: f chunks 3 WV .. 3 WV + 2 (LDS order,
 // so the source chunk carries the swizzle), plus dlp (wave 0), dlm (wave 1), gadd (waves 2, 3;
 // samples n0 .. n0 + 4 of the tile's rows, clamped to the buffer); without dlm / gadd a wave
-// re-loads a valid address into the unused space so that every wave issues four
+// re-loads a valid address into the unused space so that every wave issues four. A full tile
+// addresses its rows from a wave-uniform base (SGPRs) plus this lane's fixed offset (foff);
+// the last, partial tile clamps its rows to M - 1 with 64-bit per-lane addresses.
 template <typename E, int WV, bool GDMA>
-__device__ __forceinline__ void heads_issue(const HeadBwdParams<E>& p, HeadSlot<E>& S, int64_t t, int lane) {
+__device__ __forceinline__ void heads_issue(const HeadBwdParams<E>& p, HeadSlot<E>& S, int64_t t, int lane,
+                                            const uint32_t (&foff)[3]) {
   const int64_t base = t * TRB, last = p.M - 1;
-  const uint32_t fb = lds_addr(S.f);
+  const uint32_t fb = __builtin_amdgcn_readfirstlane(lds_addr(S.f));
+  const uint32_t db = __builtin_amdgcn_readfirstlane(lds_addr(S.dl[WV & 1]));
+  const uint32_t gb = __builtin_amdgcn_readfirstlane(lds_addr(S.ga) + (WV & 1) * 1024);
+  if (base + TRB <= p.M) {
+    const E* fbase = p.f + base * C;
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const int lc = (3 * WV + j) * 64 + lane, r = lc / 12, chs = lc - r * 12, ch = chs ^ ((r >> 2) & 3);
-    const int64_t row = base + r < p.M ? base + r : last;
-    dma_x4(p.f + row * C + ch * 8, fb + (3 * WV + j) * 1024);
-  }
-  const int64_t rowl = base + lane < p.M ? base + lane : last;
-  if constexpr (WV == 0) {
-    dma_x1(p.dlp + rowl, lds_addr(S.dl[0]));
-  } else if constexpr (WV == 1) {
-    dma_x1((p.dlm ? p.dlm : p.dlp) + rowl, lds_addr(S.dl[1]));
+    for (int j = 0; j < 3; ++j) dma_x4_s(fbase, foff[j], fb + (3 * WV + j) * 1024);
+    if constexpr (WV < 2) {
+      dma_x1_s((WV == 0 || !p.dlm ? p.dlp : p.dlm) + base, lane * 4, db);
+    }
   } else {
-    const void* src = p.f;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int lc = (3 * WV + j) * 64 + lane, r = lc / 12, chs = lc - r * 12, ch = chs ^ ((r >> 2) & 3);
+      const int64_t row = base + r < p.M ? base + r : last;
+      dma_x4(p.f + row * C + ch * 8, fb + (3 * WV + j) * 1024);
+    }
+    if constexpr (WV < 2) {
+      const int64_t rowl = base + lane < p.M ? base + lane : last;
+      dma_x1((WV == 0 || !p.dlm ? p.dlp : p.dlm) + rowl, db);
+    }
+  }
+  if constexpr (WV >= 2) {
     if (GDMA) {
       const int64_t nfl = (p.M / p.P) * C;  // gadd floats
       int64_t q = (base / p.P) * C + (WV - 2) * 256 + lane * 4;
       q = q + 4 <= nfl ? q : nfl - 4;
-      src = p.gadd + q;
+      dma_x4(p.gadd + q, gb);
+    } else {
+      dma_x4_s(p.f, lane * 16, gb);
     }
-    dma_x4(src, lds_addr(S.ga) + (WV - 2) * 1024);
   }
 }
 
@@ -265,18 +287,41 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
   constexpr int PT = WV & 1, HD = WV >> 1;
   constexpr int KT0 = WV < 2 ? 0 : 2, NKT = WV < 2 ? 2 : 1;  // df k-tiles
   constexpr int T0 = WV < 2 ? 4 * WV : 8 + 5 * (WV - 2), NTW = WV < 2 ? 4 : 5;  // dW1 tiles
+  constexpr int CT0 = T0 / 3, CT1 = (T0 + NTW - 1) / 3;  // c-tiles of this wave's dW1 tiles
+  // db1 c-tiles (each c-tile in exactly one wave, among its dW1 c-tiles): {0,1} {2} {3} {4,5}
+  constexpr int B0 = WV == 0 ? 0 : (WV == 1 ? 2 : (WV == 2 ? 3 : 4)), NB = (WV == 0 || WV == 3) ? 2 : 1;
   const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hh = lane >> 5;
   const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-  f32x16 dwacc[NTW];
+  f32x16 dwacc[NTW], dbacc[NB];
 #pragma unroll
   for (int t = 0; t < NTW; ++t)
 #pragma unroll
     for (int i = 0; i < 16; ++i) dwacc[t][i] = 0.f;
-  float dw2a[3][16], db1a[3][16];  // channel (3 HD + j) * 32 + 8 (r >> 2) + 4 hh + (r & 3), this lane's pixels
+#pragma unroll
+  for (int t = 0; t < NB; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dbacc[t][i] = 0.f;
+  float dw2a[3][16];  // channel (3 HD + j) * 32 + 8 (r >> 2) + 4 hh + (r & 3), this lane's pixels
 #pragma unroll
   for (int j = 0; j < 3; ++j)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) dw2a[j][r] = db1a[j][r] = 0.f;
+    for (int r = 0; r < 16; ++r) dw2a[j][r] = 0.f;
+  // b1 in the H accumulators' layout: the first MFMA of each chain starts from it (h = W1 f + b1)
+  f32x16 b1i[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) b1i[j][r] = p.b1[(3 * HD + j) * 32 + 8 * (r >> 2) + 4 * hh + (r & 3)];
+  E8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (E)1.0f;
+  uint32_t foff[3];  // this lane's f chunks of a full tile: byte offsets from the tile's first row
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int lc = (3 * WV + j) * 64 + lane, r = lc / 12, chs = lc - r * 12, ch = chs ^ ((r >> 2) & 3);
+    foff[j] = (uint32_t)((r * C + ch * 8) * 2);
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): b1 is in registers before the ring's DMAs start
 
   const int64_t ntiles = (p.M + TRB - 1) / TRB;
   const int nloc = (int)((ntiles - blockIdx.x + gridDim.x - 1) / gridDim.x);  // tiles of this workgroup
@@ -284,13 +329,14 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
   unsigned long long dacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long tlast = __builtin_amdgcn_s_memtime();
 #endif
-  for (int i = 0; i + 1 < NS && i < nloc; ++i) heads_issue<E, WV, GDMA>(p, L.ring[i], blockIdx.x + (int64_t)i * gridDim.x, lane);
+  for (int i = 0; i + 1 < NS && i < nloc; ++i)
+    heads_issue<E, WV, GDMA>(p, L.ring[i], blockIdx.x + (int64_t)i * gridDim.x, lane, foff);
   const bool mine_dl = HD == 0 || p.dlm != nullptr;
   for (int i = 0; i < nloc; ++i) {
     const int64_t tile = blockIdx.x + (int64_t)i * gridDim.x, base = tile * TRB;
     HSTAMP(7);
     if (i + NS - 1 < nloc) {
-      heads_issue<E, WV, GDMA>(p, L.ring[(i + NS - 1) % NS], tile + (int64_t)(NS - 1) * gridDim.x, lane);
+      heads_issue<E, WV, GDMA>(p, L.ring[(i + NS - 1) % NS], tile + (int64_t)(NS - 1) * gridDim.x, lane, foff);
       HSTAMP(0);
       wait_tile<0>(i);
     } else {
@@ -303,41 +349,49 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
     const HeadSlot<E>& S = L.ring[i % NS];
     const int zo = opaque0();
 
-    // ---- H^T for this head's 96 channels and px-tile PT; dh -> LDS; dw2 / db1 in-lane ----
+    // ---- H^T (+ b1) for this head's 96 channels and px-tile PT; dh -> LDS; dw2 in-lane ----
     {
-      f32x16 acc[3];
+      const int px = PT * 32 + l32;
+      f32x4 w2r[3][4];  // w2 of this lane's channels, read before the MFMAs finish
 #pragma unroll
       for (int j = 0; j < 3; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-      const int px = PT * 32 + l32;
+        for (int g4 = 0; g4 < 4; ++g4) w2r[j][g4] = L.w2v[((3 * HD + j) * 32 + 8 * g4 + 4 * hh) / 4 + zo];
+      const float dl = (base + px < p.M && mine_dl) ? S.dl[HD][px] : 0.f;
+      f32x16 acc[3];
+      // operands double-buffered, order pinned: step ks+1's LDS reads before step ks's MFMAs
+      E8 Af[2][3], Bf[2];
+      auto ld = [&](int ks, E8 (&a)[3], E8& bb) {
+        bb = *reinterpret_cast<const E8*>(&S.f[sf_off(px, ks * 16 + 8 * hh) + zo]);
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          a[j] = *reinterpret_cast<const E8*>(&L.w[((3 * HD + j) * 32 + l32) * WP + ks * 16 + 8 * hh + zo]);
+      };
+      ld(0, Af[0], Bf[0]);
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
       for (int ks = 0; ks < 6; ++ks) {
-        const E8 b = *reinterpret_cast<const E8*>(&S.f[sf_off(px, ks * 16 + 8 * hh) + zo]);
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const E8 a = *reinterpret_cast<const E8*>(&L.w[((3 * HD + j) * 32 + l32) * WP + ks * 16 + 8 * hh + zo]);
-          acc[j] = mfma32(a, b, acc[j]);
+        if (ks + 1 < 6) {
+          ld(ks + 1, Af[(ks + 1) & 1], Bf[(ks + 1) & 1]);
+          __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
         }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[j] = mfma32(Af[ks & 1][j], Bf[ks & 1], ks == 0 ? b1i[j] : acc[j]);
+        __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
       }
-      const float dl = (base + px < p.M && mine_dl) ? S.dl[HD][px] : 0.f;
+      // h = max(acc, 0); dw2 += h dl = acc (dl if acc > 0 else 0); dh = (dl if acc > 0 else 0) w2
 #pragma unroll
       for (int j = 0; j < 3; ++j)
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
           const int c0 = (3 * HD + j) * 32 + 8 * g4 + 4 * hh;
-          const float4 bb = *reinterpret_cast<const float4*>(&L.b1[c0 + zo]);
-          const float4 ww = *reinterpret_cast<const float4*>(&L.w2[c0 + zo]);
-          const float bv[4] = {bb.x, bb.y, bb.z, bb.w}, wv[4] = {ww.x, ww.y, ww.z, ww.w};
           E4 d4;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int r = 4 * g4 + e;
-            const float hv = fmaxf(acc[j][r] + bv[e], 0.f);
-            dw2a[j][r] += hv * dl;
-            const float dh = hv > 0.f ? dl * wv[e] : 0.f;
-            db1a[j][r] += dh;
-            d4[e] = (E)dh;
+            const float t = acc[j][r] > 0.f ? dl : 0.f;
+            dw2a[j][r] = __builtin_fmaf(acc[j][r], t, dw2a[j][r]);
+            d4[e] = (E)(t * w2r[j][g4][e]);
           }
           *reinterpret_cast<E4*>(&L.dh[sd_off(px, c0)]) = d4;
         }
@@ -370,16 +424,28 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
 #pragma unroll
           for (int r = 0; r < 16; ++r) acc2[u][r] = 0.f;
       }
-#pragma unroll
-      for (int ks = 0; ks < 6; ++ks) {
-        const E8 b = *reinterpret_cast<const E8*>(&L.dh[sd_off(rb, ks * 16 + 8 * hh) + zo]);
+      // operands double-buffered, order pinned: step ks+1's LDS reads before step ks's MFMAs
+      E8 A[2][NKT], Bv[2];
+      auto ld = [&](int ks, E8 (&a)[NKT], E8& bb) {
+        bb = *reinterpret_cast<const E8*>(&L.dh[sd_off(rb, ks * 16 + 8 * hh) + zo]);
         const int r0 = ks * 16 + 8 * (g >> 1) + q + zo;  // W1 rows (K = c), transposed read
 #pragma unroll
         for (int u = 0; u < NKT; ++u) {
           const int col = (KT0 + u) * 32 + 16 * (g & 1) + 4 * pp;
-          const E8 a = cat8(lds_tr4(&L.w[r0 * WP + col]), lds_tr4(&L.w[(r0 + 4) * WP + col]));
-          acc2[u] = mfma32(a, b, acc2[u]);
+          a[u] = cat8(lds_tr4(&L.w[r0 * WP + col]), lds_tr4(&L.w[(r0 + 4) * WP + col]));
         }
+      };
+      ld(0, A[0], Bv[0]);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1 + 2 * NKT, 0);
+#pragma unroll
+      for (int ks = 0; ks < 6; ++ks) {
+        if (ks + 1 < 6) {
+          ld(ks + 1, A[(ks + 1) & 1], Bv[(ks + 1) & 1]);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1 + 2 * NKT, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < NKT; ++u) acc2[u] = mfma32(A[ks & 1][u], Bv[ks & 1], acc2[u]);
+        __builtin_amdgcn_sched_group_barrier(0x008, NKT, 0);
       }
       // acc2[u][r] = df[px = rb][k = (KT0 + u) * 32 + 8 (r >> 2) + 4 hh + (r & 3)]
 #pragma unroll
@@ -390,25 +456,39 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
               E4{(E)acc2[u][4 * gg + 0], (E)acc2[u][4 * gg + 1], (E)acc2[u][4 * gg + 2], (E)acc2[u][4 * gg + 3]};
     }
     HSTAMP(4);
-    // ---- dW1[c][k] += sum_px dh[px][c] f[px][k] over the tile's 64 rows ----
+    // ---- dW1[c][k] += sum_px dh[px][c] f[px][k]; db1[c] += sum_px dh[px][c] (B = ones) ----
+    {
+      constexpr int NA = CT1 - CT0 + 1;
+      E8 av[2][NA], bv[2][3];
+      auto ld = [&](int kk, E8 (&a)[NA], E8 (&b)[3]) {
+        const int r0 = kk * 16 + 8 * (g >> 1) + q + zo;
 #pragma unroll
-    for (int kk = 0; kk < TRB / 16; ++kk) {
-      const int r0 = kk * 16 + 8 * (g >> 1) + q + zo;
-      E8 av[6], bv[3];
+        for (int ct = CT0; ct <= CT1; ++ct) {
+          const int col = ct * 32 + 16 * (g & 1) + 4 * pp;
+          a[ct - CT0] = cat8(lds_tr4(&L.dh[sd_off(r0, col)]), lds_tr4(&L.dh[sd_off(r0 + 4, col)]));
+        }
 #pragma unroll
-      for (int ct = T0 / 3; ct <= (T0 + NTW - 1) / 3; ++ct) {
-        const int col = ct * 32 + 16 * (g & 1) + 4 * pp;
-        av[ct] = cat8(lds_tr4(&L.dh[sd_off(r0, col)]), lds_tr4(&L.dh[sd_off(r0 + 4, col)]));
-      }
+        for (int kt = 0; kt < 3; ++kt) {
+          const int col = kt * 32 + 16 * (g & 1) + 4 * pp;
+          b[kt] = cat8(lds_tr4(&S.f[sf_off(r0, col)]), lds_tr4(&S.f[sf_off(r0 + 4, col)]));
+        }
+      };
+      ld(0, av[0], bv[0]);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * (NA + 3), 0);
 #pragma unroll
-      for (int kt = 0; kt < 3; ++kt) {
-        const int col = kt * 32 + 16 * (g & 1) + 4 * pp;
-        bv[kt] = cat8(lds_tr4(&S.f[sf_off(r0, col)]), lds_tr4(&S.f[sf_off(r0 + 4, col)]));
-      }
+      for (int kk = 0; kk < TRB / 16; ++kk) {
+        if (kk + 1 < TRB / 16) {
+          ld(kk + 1, av[(kk + 1) & 1], bv[(kk + 1) & 1]);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2 * (NA + 3), 0);
+        }
 #pragma unroll
-      for (int t = 0; t < NTW; ++t) {
-        const int tt = T0 + t;
-        dwacc[t] = mfma32(av[tt / 3], bv[tt % 3], dwacc[t]);
+        for (int t = 0; t < NTW; ++t) {
+          const int tt = T0 + t;
+          dwacc[t] = mfma32(av[kk & 1][tt / 3 - CT0], bv[kk & 1][tt % 3], dwacc[t]);
+        }
+#pragma unroll
+        for (int t = 0; t < NB; ++t) dbacc[t] = mfma32(av[kk & 1][B0 + t - CT0], ones, dbacc[t]);
+        __builtin_amdgcn_sched_group_barrier(0x008, NTW + NB, 0);
       }
     }
     HSTAMP(5);
@@ -426,8 +506,9 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
   if (p.diag && lane == 0)
     for (int k = 0; k < 8; ++k) p.diag[((size_t)blockIdx.x * 4 + WV) * 8 + k] = dacc[k];
 #endif
-  // ---- partials: dW1 tiles; dw2 / db1 summed over the lanes (pixels), the two px-tile waves
-  // of a head combined in fixed order by the caller (LDS: the dh region) ----
+  // ---- partials: dW1 tiles, db1 (column 0 of the ones products: lanes 0 and 32), dw2 summed
+  // over the lanes (pixels); the two px-tile waves of a head combine dw2 in fixed order
+  // through LDS (the dh region) in the caller ----
   float* part = p.part + (size_t)blockIdx.x * PART;
 #pragma unroll
   for (int t = 0; t < NTW; ++t) {
@@ -438,26 +519,25 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
       part[c * C + kt * 32 + l32] = dwacc[t][r];
     }
   }
+  if (l32 == 0) {
+#pragma unroll
+    for (int t = 0; t < NB; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) part[NH * C + NH + (B0 + t) * 32 + 8 * (r >> 2) + 4 * hh + (r & 3)] = dbacc[t][r];
+  }
 #pragma unroll
   for (int j = 0; j < 3; ++j)
 #pragma unroll
     for (int r = 0; r < 16; ++r)
 #pragma unroll
-      for (int o = 1; o < 32; o <<= 1) {
-        dw2a[j][r] += __shfl_xor(dw2a[j][r], o);
-        db1a[j][r] += __shfl_xor(db1a[j][r], o);
-      }
+      for (int o = 1; o < 32; o <<= 1) dw2a[j][r] += __shfl_xor(dw2a[j][r], o);
   lds_barrier();  // the dh region is free
-  float* red = reinterpret_cast<float*>(L.dh);  // [2 pt][2][NH]
+  float* red = reinterpret_cast<float*>(L.dh);  // [2 pt][NH]
   if (l32 == 0) {
 #pragma unroll
     for (int j = 0; j < 3; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int c = (3 * HD + j) * 32 + 8 * (r >> 2) + 4 * hh + (r & 3);
-        red[(PT * 2 + 0) * NH + c] = dw2a[j][r];
-        red[(PT * 2 + 1) * NH + c] = db1a[j][r];
-      }
+      for (int r = 0; r < 16; ++r) red[PT * NH + (3 * HD + j) * 32 + 8 * (r >> 2) + 4 * hh + (r & 3)] = dw2a[j][r];
   }
 }
 
@@ -470,10 +550,7 @@ __global__ __launch_bounds__(256, 1) void k_heads_bwd(HeadBwdParams<E> p) {
     const int c = i / 12, k8 = i - c * 12;
     *reinterpret_cast<u32x4*>(&L.w[c * WP + k8 * 8]) = *reinterpret_cast<const u32x4*>(&p.w1[c * C + k8 * 8]);
   }
-  for (int i = tid; i < NH; i += 256) {
-    L.b1[i] = p.b1[i];
-    L.w2[i] = p.w2[i];
-  }
+  for (int i = tid; i < NH / 4; i += 256) L.w2v[i] = reinterpret_cast<const f32x4*>(p.w2)[i];
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the staging loads are done before the DMAs start
   __syncthreads();
   switch (__builtin_amdgcn_readfirstlane(tid >> 6)) {
@@ -485,10 +562,7 @@ __global__ __launch_bounds__(256, 1) void k_heads_bwd(HeadBwdParams<E> p) {
   __syncthreads();
   const float* red = reinterpret_cast<const float*>(L.dh);
   float* part = p.part + (size_t)blockIdx.x * PART;
-  for (int i = tid; i < NH; i += 256) {
-    part[NH * C + i] = red[0 * NH + i] + red[2 * NH + i];
-    part[NH * C + NH + i] = red[1 * NH + i] + red[3 * NH + i];
-  }
+  for (int i = tid; i < NH; i += 256) part[NH * C + i] = red[i] + red[NH + i];
 }
 
 // Sum of the G partials, deterministic (as k_reduce in mscnn_bwd.hip): a 256-thread block covers

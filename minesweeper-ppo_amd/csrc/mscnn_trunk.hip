@@ -389,6 +389,321 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_fwd(TrunkFwdPar
 #endif
 }
 
+// k_trunk_fwd2 (boards of <= 256 cells): one 512-thread workgroup per CU runs TWO samples, one per
+// 4-wave team, through the same code in lockstep: the teams share each weight tap, which is staged
+// once for both into a double buffer, so a tap costs one barrier instead of two and its hand-off
+// overlaps the MFMAs (k_trunk_fwd: one sample per 256-thread workgroup, two workgroups per CU, one
+// weight buffer each). Per-sample arithmetic is k_trunk_fwd's, so the outputs are bitwise equal.
+// LDS: sX [2 teams][P+1][104] | sW [2 taps][96][104] | sRed [2][4][6] | sAB [2][3][96].
+__host__ __device__ inline size_t tf2_lds(int P) {
+  return (size_t)2 * tf_region(P) * 2 + (size_t)2 * COUT * CINP * 2 + 2 * WAVES * NGRP * 4 + 2 * 3 * COUT * 4;
+}
+constexpr int NWC2 = (COUT * C8 + 511) / 512;  // 16-B chunks of a weight tap per thread of 512
+template <typename E>
+__device__ __forceinline__ void load_wtap2(const E* wt, int tap, int tid, u32x4 (&v)[NWC2]) {
+  const u32x4* ws = reinterpret_cast<const u32x4*>(wt + (size_t)tap * COUT * COUT);
+#pragma unroll
+  for (int k = 0; k < NWC2; ++k) {
+    const int i = tid + 512 * k;
+    if (k < COUT * C8 / 512 || i < COUT * C8) v[k] = ws[i];
+  }
+}
+template <typename E>
+__device__ __forceinline__ void store_wtap2(E* sW, int tid, const u32x4 (&v)[NWC2]) {
+#pragma unroll
+  for (int k = 0; k < NWC2; ++k) {
+    const int i = tid + 512 * k;
+    if (k < COUT * C8 / 512 || i < COUT * C8) {
+      const int r = i / C8, c = i - r * C8;
+      *reinterpret_cast<u32x4*>(&sW[r * CINP + c * 8]) = v[k];
+    }
+  }
+}
+template <typename E, int NPT, bool FULL>
+__global__ __launch_bounds__(512, 1) void k_trunk_fwd2(TrunkFwdParams<E> p) {
+  // no contraction: every expression rounds the same way in the per-layer and the one-launch
+  // kernels (explicit fmaf where a fused multiply-add is wanted), so they agree bitwise
+#pragma clang fp contract(off)
+  typedef typename EV<E>::v8 E8;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NEC = (NPT * 128 * C8 + 255) / 256;  // 16-B chunks of a sample tile per thread
+  const int H = p.H, W = p.W, P = H * W;
+  const int team = threadIdx.x >> 8;
+  E* sX = reinterpret_cast<E*>(smem) + team * tf_region(P);
+  E* sW0 = reinterpret_cast<E*>(smem) + 2 * tf_region(P);  // weight tap t in buffer t & 1
+  float* sRed = reinterpret_cast<float*>(sW0 + 2 * COUT * CINP) + team * WAVES * NGRP;
+  float* sAB = reinterpret_cast<float*>(sW0 + 2 * COUT * CINP) + 2 * WAVES * NGRP + team * 3 * COUT;
+  const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const float inv_cnt = 1.0f / (16.0f * (float)P);
+
+  int qr[NPT], qc[NPT];  // this lane's output pixel of each 32-pixel tile
+#pragma unroll
+  for (int t = 0; t < NPT; ++t) {
+    const int q = (wave * NPT + t) * 32 + l32;
+    qr[t] = q < P ? q / W : -1000;  // a pixel past P reads the zero row at every tap
+    qc[t] = q < P ? q - qr[t] * W : -1000;
+  }
+  u32x4 wr[NWC2];
+#ifdef MC_DIAG
+  unsigned long long dacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tlast = __builtin_amdgcn_s_memtime();
+#endif
+
+  // team t of workgroup b takes samples 2 (b + k G) + t; an odd N leaves team 1 of the last pair
+  // without one: it runs sample N - 1 alongside team 0 (every barrier is the workgroup's) and stores
+  // nothing
+  for (int pair = blockIdx.x; 2 * pair < p.N; pair += gridDim.x) {
+    const bool valid = 2 * pair + team < p.N;
+    const int n = valid ? 2 * pair + team : p.N - 1;
+    const size_t so = (size_t)n * P * COUT;  // this sample's offset in every [N][P][96] tensor
+    E* wsl = p.ws + ((size_t)blockIdx.x * 2 + team) * P * COUT;  // this team's workspace slot
+    {  // stage block 0's input and layer 0's tap-0 weights
+      const int tid = (threadIdx.x & 255) + opaque0();
+      const int wid = threadIdx.x + opaque0();
+      u32x4 xin[NEC];
+      const u32x4* xs = reinterpret_cast<const u32x4*>(p.x0 + so);
+#pragma unroll
+      for (int k = 0; k < NEC; ++k) {
+        const int i = tid + 256 * k;
+        if (FULL || i < P * C8) xin[k] = xs[i];
+      }
+      load_wtap2<E>(p.L[0].wt, 0, wid, wr);
+      for (int i = tid; i < C8; i += 256) *reinterpret_cast<u32x4*>(&sX[P * CINP + i * 8]) = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int k = 0; k < NEC; ++k) {
+        const int i = tid + 256 * k;
+        if (FULL || i < P * C8) {
+          const int px = i / C8, c8 = i - px * C8;
+          *reinterpret_cast<u32x4*>(&sX[px * CINP + c8 * 8]) = xin[k];
+        }
+      }
+      store_wtap2<E>(sW0, wid, wr);
+    }
+    __syncthreads();
+
+    for (int l = 0; l < p.NL; ++l) {
+      // loop-variant thread coordinates: the per-chunk address math and the taps' row offsets
+      // are recomputed per layer instead of hoisted out of this loop (they would be spilled)
+      const int tid = (threadIdx.x & 255) + opaque0();
+      const int wid = threadIdx.x + opaque0();
+#pragma unroll
+      for (int t = 0; t < NPT; ++t) asm volatile("" : "+v"(qr[t]), "+v"(qc[t]));
+      const E* wt = p.L[l].wt;
+      float biasv[3];
+#pragma unroll
+      for (int ct = 0; ct < 3; ++ct) biasv[ct] = p.L[l].bias[ct * 32 + l32];
+
+      f32x16 acc[NPT][3];
+#pragma unroll
+      for (int t = 0; t < NPT; ++t)
+#pragma unroll
+        for (int ct = 0; ct < 3; ++ct)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) acc[t][ct][i] = 0.f;
+
+      TSTAMP(0);
+      for (int tap = 0; tap < 9; ++tap) {
+        if (tap + 1 < 9) load_wtap2<E>(wt, tap + 1, wid, wr);
+        const E* sW = sW0 + (tap & 1) * COUT * CINP;
+        const int dr = tap / 3 - 1, dc = tap % 3 - 1;
+        int aoff[NPT];
+#pragma unroll
+        for (int t = 0; t < NPT; ++t) {
+          const int sr = qr[t] + dr, sc = qc[t] + dc;
+          const bool v = (unsigned)sr < (unsigned)H && (unsigned)sc < (unsigned)W;
+          aoff[t] = (v ? sr * W + sc : P) * CINP + 8 * hh;
+        }
+        // 6 k steps, operands double-buffered, order pinned: step k+1's LDS reads before step k's MFMAs
+        constexpr int KS = COUT / 16;
+        E8 A[2][NPT], B[2][3];
+        auto ld = [&](int ks, E8 (&a)[NPT], E8 (&b)[3]) {
+#pragma unroll
+          for (int ct = 0; ct < 3; ++ct)
+            b[ct] = *reinterpret_cast<const E8*>(&sW[(ct * 32 + l32) * CINP + ks * 16 + 8 * hh]);
+#pragma unroll
+          for (int t = 0; t < NPT; ++t) a[t] = *reinterpret_cast<const E8*>(&sX[aoff[t] + ks * 16]);
+        };
+        ld(0, A[0], B[0]);
+        __builtin_amdgcn_sched_group_barrier(0x100, NPT + 3, 0);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          if (ks + 1 < KS) {
+            ld(ks + 1, A[(ks + 1) & 1], B[(ks + 1) & 1]);
+            __builtin_amdgcn_sched_group_barrier(0x100, NPT + 3, 0);
+          }
+#pragma unroll
+          for (int t = 0; t < NPT; ++t)
+#pragma unroll
+            for (int ct = 0; ct < 3; ++ct) acc[t][ct] = mfma32(A[ks & 1][t], B[ks & 1][ct], acc[t][ct]);
+          __builtin_amdgcn_sched_group_barrier(0x008, 3 * NPT, 0);
+        }
+        // tap + 1 into the other buffer (last read by tap - 1, before the previous barrier)
+        if (tap + 1 < 9) store_wtap2<E>(sW0 + ((tap + 1) & 1) * COUT * CINP, wid, wr);
+        lds_barrier();  // tap + 1 visible; this tap's buffer (and after the last tap sX) fully read
+      }
+      TSTAMP(1);
+      // the next layer's tap-0 weights: loaded now, written to sW (free) after the statistics
+      const bool more = l + 1 < p.NL;
+      if (more) load_wtap2<E>(p.L[l + 1].wt, 0, wid, wr);
+
+      // ---------------- GroupNorm statistics (two-pass, as the per-layer kernel) ----------------
+      float gmean[NGRP], grstd[NGRP];
+      for (int pass = 0; pass < 2; ++pass) {
+        float part[3];
+#pragma unroll
+        for (int ct = 0; ct < 3; ++ct) {
+          const float mu = pass ? gmean[2 * ct + (l32 >> 4)] : 0.f;
+          float v[NPT * 16];
+#pragma unroll
+          for (int t = 0; t < NPT; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const int px = (wave * NPT + t) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+              const float d = acc[t][ct][i] + biasv[ct] - mu;
+              v[t * 16 + i] = (FULL || px < P) ? (pass ? d * d : d) : 0.f;
+            }
+#pragma unroll
+          for (int w2 = NPT * 8; w2 >= 1; w2 >>= 1)
+#pragma unroll
+            for (int i = 0; i < w2; ++i) v[i] += v[i + w2];
+          part[ct] = row_sum16(v[0]);
+        }
+        float gs[3][2];
+#pragma unroll
+        for (int ct = 0; ct < 3; ++ct) {
+          gs[ct][0] = readlane_f(part[ct], 15) + readlane_f(part[ct], 47);
+          gs[ct][1] = readlane_f(part[ct], 31) + readlane_f(part[ct], 63);
+        }
+        if (lane == 0) {
+#pragma unroll
+          for (int ct = 0; ct < 3; ++ct) {
+            sRed[wave * NGRP + 2 * ct] = gs[ct][0];
+            sRed[wave * NGRP + 2 * ct + 1] = gs[ct][1];
+          }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int g = 0; g < NGRP; ++g) {
+          float tot = 0.f;
+#pragma unroll
+          for (int w = 0; w < WAVES; ++w) tot += sRed[w * NGRP + g];
+          if (pass == 0) gmean[g] = tot * inv_cnt;
+          else grstd[g] = rsqrtf(tot * inv_cnt + p.eps);
+        }
+        __syncthreads();  // sRed reused by the next pass
+      }
+      TSTAMP(2);
+      float* stats = p.L[l].stats;
+      if (stats && valid && tid < NGRP) {
+        float m = 0.f, r = 0.f;
+#pragma unroll
+        for (int g = 0; g < NGRP; ++g)
+          if (g == tid) {
+            m = gmean[g];
+            r = grstd[g];
+          }
+        stats[((size_t)n * NGRP + tid) * 2 + 0] = m;
+        stats[((size_t)n * NGRP + tid) * 2 + 1] = r;
+      }
+      // y -> LDS over the (fully read) input tile, in the tile's padded layout
+#pragma unroll
+      for (int ct = 0; ct < 3; ++ct)
+#pragma unroll
+        for (int t = 0; t < NPT; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int px = (wave * NPT + t) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+            if (FULL || px < P) sX[px * CINP + ct * 32 + l32] = (E)(acc[t][ct][i] + biasv[ct]);
+          }
+      if (more) store_wtap2<E>(sW0, wid, wr);  // buffer 0: last read by tap 8
+      if (tid < COUT) {  // z = y * scale + shift (+ res), then ReLU, then * dropout scale
+        const int g = tid >> 4;
+        float mu = 0.f, rs = 0.f;
+#pragma unroll
+        for (int gg = 0; gg < NGRP; ++gg)
+          if (gg == g) {
+            mu = gmean[gg];
+            rs = grstd[gg];
+          }
+        const float a = p.L[l].gamma[tid] * rs;
+        sAB[tid] = a;
+        sAB[COUT + tid] = p.L[l].beta[tid] - mu * a;
+        const float* dmask = p.L[l].dmask;
+        sAB[2 * COUT + tid] = dmask ? dmask[(size_t)n * COUT + tid] : 1.0f;
+      }
+      __syncthreads();
+      TSTAMP(3);
+
+      // ---------------- epilogue: 16-B chunks of [px][co], written in place ----------------
+      // residual (conv2 of block b): the block input = block 0's input, or block b-1's output
+      const E* res = nullptr;
+      if (l & 1) {
+        if (l == 1) res = p.x0 + so;
+        else res = !valid ? p.x0 + so : (p.L[l - 2].out ? p.L[l - 2].out + so : wsl);
+      }
+      // a team without a sample stores nothing (its residuals come from x0: any valid address;
+      // with saved outputs there is no workspace)
+      E* out = !valid ? nullptr : (p.L[l].out ? p.L[l].out + so : ((l & 1) && more ? wsl : nullptr));
+      E* ysave = p.L[l].ysave && valid ? p.L[l].ysave + so : nullptr;
+      uint8_t* rmask = p.L[l].rmask && valid ? p.L[l].rmask + (size_t)n * P * C8 : nullptr;
+      float ca[3][8], cb[3][8], cd[3][8];
+#pragma unroll
+      for (int j3 = 0; j3 < 3; ++j3) {
+        const int cg = ((tid % C8) + 4 * j3) % C8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          ca[j3][j] = sAB[cg * 8 + j];
+          cb[j3][j] = sAB[COUT + cg * 8 + j];
+          cd[j3][j] = sAB[2 * COUT + cg * 8 + j];
+        }
+      }
+      // residual chunks are loaded RB at a time, all of a batch before its first store (a load
+      // issued after a store waits for that store too: vmcnt counts both)
+      constexpr int RB = (NEC + 1) / 2;
+      u32x4 rq[RB];
+#pragma unroll
+      for (int k = 0; k < NEC; ++k) {
+        const int c = tid + 256 * k;
+        if (k % RB == 0) {
+#pragma unroll
+          for (int u = 0; u < RB; ++u) {
+            const int cu = tid + 256 * (k + u);
+            rq[u] = u32x4{0u, 0u, 0u, 0u};
+            if (res && k + u < NEC && (FULL || cu < P * C8)) rq[u] = *reinterpret_cast<const u32x4*>(&res[(size_t)cu * 8]);
+          }
+        }
+        if (FULL || c < P * C8) {
+          const int px = c / C8, c8 = c - px * C8;
+          E* sp = &sX[px * CINP + c8 * 8];
+          const u32x4 yv = *reinterpret_cast<const u32x4*>(sp);
+          if (ysave) *reinterpret_cast<u32x4*>(&ysave[(size_t)c * 8]) = yv;
+          const E8 y8 = __builtin_bit_cast(E8, yv);
+          const E8 r8 = __builtin_bit_cast(E8, rq[k % RB]);
+          E8 o8;
+          uint32_t mb = 0u;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float z = fmaxf(__builtin_fmaf((float)y8[j], ca[k % 3][j], cb[k % 3][j]) + (float)r8[j], 0.f);
+            o8[j] = (E)(z * cd[k % 3][j]);
+            mb |= ((float)o8[j] > 0.f ? 1u : 0u) << j;
+          }
+          const u32x4 ov = __builtin_bit_cast(u32x4, o8);
+          if (out) *reinterpret_cast<u32x4*>(&out[(size_t)c * 8]) = ov;
+          if (rmask) rmask[c] = (uint8_t)mb;
+          *reinterpret_cast<u32x4*>(sp) = ov;  // the next layer's input
+        }
+      }
+      __syncthreads();  // the tile and sAB are complete / free
+      TSTAMP(4);
+    }
+  }
+#ifdef MC_DIAG
+  if (p.diag && (threadIdx.x & 63) == 0 && team == 0)
+    for (int k = 0; k < 8; ++k) p.diag[((size_t)blockIdx.x * 4 + wave) * 8 + k] = dacc[k];
+#endif
+}
+
 // ------------------------------------------------------------------------------------
 template <typename E>
 struct TBLayer {
@@ -775,6 +1090,17 @@ int trunk_grid(int n, size_t lds) {
   const int cap = per_cu * num_cus();
   return n < cap ? n : cap;
 }
+// k_trunk_fwd2 (P <= 256): one 512-thread workgroup per CU, two samples each
+inline bool fwd_two(int P) { return P <= 256; }
+int trunk_grid2(int n) {
+  const int pairs = (n + 1) / 2, cap = num_cus();
+  return pairs < cap ? pairs : cap;
+}
+// workspace slots of the forward: one per sample in flight (either kernel)
+int64_t fwd_slots(int n, int P) {
+  const int64_t one = trunk_grid(n, tf_lds(P)), two = fwd_two(P) ? 2 * (int64_t)trunk_grid2(n) : 0;
+  return one > two ? one : two;
+}
 // the backward's partial rows: mscnn_bwd.hip make_plan's grid_d
 int trunk_vgrid(int n) { return n < 2 * num_cus() ? n : 2 * num_cus(); }
 
@@ -808,6 +1134,14 @@ int launch_trunk_fwd(const TrunkFwdParams<E>& p, hipStream_t s) {
   return launched("k_trunk_fwd");
 }
 
+template <typename E, int NPT, bool FULL>
+int launch_trunk_fwd2(const TrunkFwdParams<E>& p, hipStream_t s) {
+  static bool attr = false;
+  lds_attr_once(k_trunk_fwd2<E, NPT, FULL>, attr);
+  hipLaunchKernelGGL((k_trunk_fwd2<E, NPT, FULL>), dim3(trunk_grid2(p.N)), dim3(512), tf2_lds(p.H * p.W), s, p);
+  return launched("k_trunk_fwd2");
+}
+
 template <typename E>
 int run_trunk_fwd(const uint16_t* x0, const mc_fwd_layer* layers, int nl, void* work, int n, int h, int w,
                   float eps, hipStream_t s) {
@@ -836,6 +1170,14 @@ int run_trunk_fwd(const uint16_t* x0, const mc_fwd_layer* layers, int nl, void* 
     p.L[l].rmask = a.relu_mask;
   }
   const int P = h * w;
+  // same-box A/B (profiles/r05/trunk_fwd2_ab.txt): the two-sample kernel is 3 % faster on the
+  // no-grad forward at 16x16 and 2-6 % at 9x9, but level with the saving forward at 16x16, whose
+  // store-heavy epilogues it runs in lockstep; the saving forward at 16x16 keeps k_trunk_fwd
+  const bool save = layers[0].ysave != nullptr;
+  if (fwd_two(P) && (!save || P <= 128)) {
+    if (P == 256) return launch_trunk_fwd2<E, 2, true>(p, s);
+    return P <= 128 ? launch_trunk_fwd2<E, 1, false>(p, s) : launch_trunk_fwd2<E, 2, false>(p, s);
+  }
   if (P == 256) return launch_trunk_fwd<E, 2, true>(p, s);
   const int npt = ((P + 31) / 32 + WAVES - 1) / WAVES;
   switch (npt) {
@@ -920,7 +1262,7 @@ void mc_set_trunk_diag(unsigned long long* fwd, unsigned long long* bwd) {
 int64_t mc_trunk_fwd_workspace(int32_t n, int32_t h, int32_t w_) {
   if (n <= 0 || h <= 0 || w_ <= 0 || h * w_ > 512) return -1;
   const int P = h * w_;
-  return (int64_t)trunk_grid(n, tf_lds(P)) * P * COUT * 2;
+  return fwd_slots(n, P) * P * COUT * 2;
 }
 
 int mc_trunk_fwd(const uint16_t* x0, const mc_fwd_layer* layers, int32_t nlayers, void* work, int64_t work_bytes,

@@ -2067,7 +2067,8 @@ __device__ __forceinline__ Pcg lr_state(const LateRng& R) {
 // MS_DIAG builds: k_late's cycle accounting (tools/late_diag.py), summed over the launch in dacc:
 // [0] whole launch, [1] envs visited, [2] late starts, [3] envs without a late start (draw + stores
 // + emit), [4] first clicks (placement included), [5] extra-click loops, [6] extra clicks,
-// [7] of them flood fills, [8] flood iterations, [9] late envs' stores + emit, [10] attempts
+// [7] of them flood fills, [8] flood iterations, [9] late envs' stores + emit, [10] attempts,
+// [14] cycles of flood fills (dilation + list rebuild), [15] cycles of flood clicks before the fill
 #ifdef MS_DIAG
 #define LSTAMP(k)                                          \
   do {                                                     \
@@ -2085,6 +2086,7 @@ __device__ __forceinline__ Pcg lr_state(const LateRng& R) {
 #define LSTAMP(k) do { } while (0)
 #define LCOUNT(k, v) do { } while (0)
 #endif
+
 
 template <int H_, int W_, class Rng>
 __device__ __forceinline__ void late_env(const KParams& p, Rng& L, const LateCfg& lc, int64_t env,
@@ -2153,12 +2155,13 @@ __device__ __forceinline__ void late_env(const KParams& p, Rng& L, const LateCfg
       uint32_t lword = 0u;
       auto build_list = [&]() {
         uint8_t* lst = reinterpret_cast<uint8_t*>(sTab);
-        uint32_t b = (uint32_t)(~mine & ~rev & (lane < H ? rowmask : 0ull));
-        uint32_t i = row_excl_scan16((uint32_t)__popc(b));
-        while (b) {
-          lst[i++] = (uint8_t)(lane * W_ + __ffs(b) - 1);
-          b &= b - 1u;
-        }
+        const uint32_t b = (uint32_t)(~mine & ~rev & (lane < H ? rowmask : 0ull));
+        const uint32_t i0 = row_excl_scan16((uint32_t)__popc(b));
+        // every column at once (predicated byte stores; a clear-lowest-bit loop is a serial,
+        // divergent chain of the lone wave): cell j of the row goes to i0 + (candidates before it)
+#pragma unroll
+        for (int j = 0; j < W_; ++j)
+          if ((b >> j) & 1u) lst[i0 + (uint32_t)__popc(b & ((1u << j) - 1u))] = (uint8_t)(lane * W_ + j);
         wave_sync();
         lword = reinterpret_cast<const uint32_t*>(lst)[lane];
         wave_sync();
@@ -2170,6 +2173,9 @@ __device__ __forceinline__ void late_env(const KParams& p, Rng& L, const LateCfg
           break;
         }
         const uint32_t cnt = (uint32_t)(safe_total - revealed);
+#ifdef MS_DIAG
+        const uint64_t ts_ = __builtin_amdgcn_s_memtime();
+#endif
         const uint32_t kk = lr_bounded(L, J, cnt - 1u);  // rng.choice(flatnonzero(...)) (row-major)
         LCOUNT(6, 1);
         int src, col;
@@ -2200,6 +2206,10 @@ __device__ __forceinline__ void late_env(const KParams& p, Rng& L, const LateCfg
             lword = (lword & keep) | (shifted & ~keep);
           }
         } else {  // flood_fill_reveal (env_numba.py:17-77) from a zero cell, as board_click
+#ifdef MS_DIAG
+          const uint64_t tf_ = __builtin_amdgcn_s_memtime();
+          LCOUNT(15, tf_ - ts_);
+#endif
           const uint64_t allow = ~mine & ~rev & (lane < H ? rowmask : 0ull);
           uint64_t Fr = (lane == src) ? (1ull << col) : 0ull;
           LCOUNT(7, 1);
@@ -2216,6 +2226,9 @@ __device__ __forceinline__ void late_env(const KParams& p, Rng& L, const LateCfg
           rev |= Fr;
           revealed += (int)wave_sum((uint32_t)__popcll(Fr));
           if constexpr (kList) build_list();
+#ifdef MS_DIAG
+          LCOUNT(14, __builtin_amdgcn_s_memtime() - tf_);
+#endif
         }
         step_count += 1;
         done = revealed >= safe_total;  // a win (env.py:133-140)

@@ -43,3 +43,4 @@ for k, name in names.items():
     print(f"  {name:40s} {tot[k] / n:8.0f} cycles per reset ({tot[k] / max(tot[0], 1) * 100:5.1f} %)")
 print(f"  extra clicks per late start {tot[6] / max(tot[2], 1):.1f}, flood fills {tot[7] / max(tot[2], 1):.1f}, "
       f"flood iterations per fill {tot[8] / max(tot[7], 1):.1f}, loop cycles per click {tot[5] / max(tot[6], 1):.0f}")
+print(f"  flood clicks: {tot[15] / max(tot[7], 1):.0f} cycles draw + select, {tot[14] / max(tot[7], 1):.0f} cycles fill + list")

@@ -427,11 +427,11 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
       // operands double-buffered, order pinned: step ks+1's LDS reads before step ks's MFMAs
       E8 A[2][NKT], Bv[2];
       auto ld = [&](int ks, E8 (&a)[NKT], E8& bb) {
-        bb = *reinterpret_cast<const E8*>(&L.dh[sd_off(rb, ks * 16 + 8 * hh) + zo]);
-        const int r0 = ks * 16 + 8 * (g >> 1) + q + zo;  // W1 rows (K = c), transposed read
+        bb = *reinterpret_cast<const E8*>(&L.dh[sd_off(rb, ks * 16 + 8 * hh)]);
+        const int r0 = ks * 16 + 8 * (g >> 1) + q;  // W1 rows (K = c), transposed read
 #pragma unroll
-        for (int u = 0; u < NKT; ++u) {
-          const int col = (KT0 + u) * 32 + 16 * (g & 1) + 4 * pp;
+        for (int u = 0; u < NKT; ++u) {  // (W1 is loop-invariant: the opaque zero keeps the reads in the loop)
+          const int col = (KT0 + u) * 32 + 16 * (g & 1) + 4 * pp + zo;
           a[u] = cat8(lds_tr4(&L.w[r0 * WP + col]), lds_tr4(&L.w[(r0 + 4) * WP + col]));
         }
       };
@@ -461,7 +461,9 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
       constexpr int NA = CT1 - CT0 + 1;
       E8 av[2][NA], bv[2][3];
       auto ld = [&](int kk, E8 (&a)[NA], E8 (&b)[3]) {
-        const int r0 = kk * 16 + 8 * (g >> 1) + q + zo;
+        // (no opaque zero here: the dh / f tiles are rewritten every tile, so nothing can be hoisted,
+        // and with a compile-time row the swizzles fold into per-lane constants + immediate offsets)
+        const int r0 = kk * 16 + 8 * (g >> 1) + q;
 #pragma unroll
         for (int ct = CT0; ct <= CT1; ++ct) {
           const int col = ct * 32 + 16 * (g & 1) + 4 * pp;
@@ -495,11 +497,13 @@ __device__ __forceinline__ void heads_bwd_body(const HeadBwdParams<E>& p, HeadLd
     lds_barrier();  // dfs complete; the slot, dh and dfs are free after the stores' reads below
     HSTAMP(2);
     // ---- df rows: 16-B chunks, whole 192-B rows (exactly HB_S stores a wave on a full tile) ----
+    E* dft = p.df + base * C;
+    const bool full = base + TRB <= p.M;
 #pragma unroll
     for (int k = 0; k < HB_S; ++k) {
       const int c = tid + 256 * k, r = c / 12, ch = c - r * 12;
       const u32x4 v = *reinterpret_cast<const u32x4*>(&L.dfs[r * DFP + ch * 8]);
-      if (base + r < p.M) *reinterpret_cast<u32x4*>(&p.df[(base + r) * C + ch * 8]) = v;
+      if (full || base + r < p.M) *reinterpret_cast<u32x4*>(&dft[c * 8]) = v;  // row r, chunk ch: c * 8
     }
   }
 #ifdef MC_DIAG

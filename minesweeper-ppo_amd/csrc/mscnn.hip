@@ -305,7 +305,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int px = (wave * NPT + t) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          if (FULL || px < P) sO[px * COUT + ct * 32 + l32] = (E)(acc[t][ct][i] + biasv[ct]);
+          if (FULL || px < P) sO[px * COUT + ct * 32 + l32] = (E)pin_f32(acc[t][ct][i] + biasv[ct]);
         }
     FSTAMP(3);  // y -> LDS
     if (tid < COUT) {  // z = y * scale + shift (+ res), then ReLU, then * dropout scale
@@ -366,7 +366,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_conv_gn_fwd(FwdParams
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float z = fmaxf(__builtin_fmaf((float)y8[j], ca[k % 3][j], cb[k % 3][j]) + (float)r8[j], 0.f);
-          o8[j] = (E)(z * cd[k % 3][j]);
+          o8[j] = (E)pin_f32(z * cd[k % 3][j]);
           mb |= ((float)o8[j] > 0.f ? 1u : 0u) << j;
         }
         *reinterpret_cast<u32x4*>(&p.out[o]) = __builtin_bit_cast(u32x4, o8);

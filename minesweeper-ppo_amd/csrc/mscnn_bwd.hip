@@ -346,7 +346,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_bwd_data(BwdDataParam
           const E8 r8 = __builtin_bit_cast(E8, ad[i]);
           E8 s8;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) s8[j] = (E)((float)a8[j] + (float)r8[j]);
+          for (int j = 0; j < 8; ++j) s8[j] = (E)pin_f32((float)a8[j] + (float)r8[j]);
           *reinterpret_cast<u32x4*>(&p.dx[((size_t)n * P + px) * COUT + c8 * 8]) = __builtin_bit_cast(u32x4, s8);
         }
       }

@@ -85,6 +85,15 @@ __device__ __forceinline__ int opaque0() {
   return z;
 }
 
+// An f32 value the compiler must materialise: (E)(a * b) and (E)(a + b) otherwise may become one
+// v_fma_mix*_f16 with a single rounding to 16 bits, chosen per call site, so two kernels
+// computing the same expression could round differently. Pinned, every such site rounds to f32
+// first and then to 16 bits, as PyTorch's f32-compute autocast does.
+__device__ __forceinline__ float pin_f32(float v) {
+  asm("" : "+v"(v));
+  return v;
+}
+
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations and
 // meets the other waves, leaving global loads and stores in flight. __syncthreads()'s
 // workgroup release fence turns into s_waitcnt vmcnt(0) as soon as global stores are

@@ -300,7 +300,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_fwd(TrunkFwdPar
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const int px = (wave * NPT + t) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-            if (FULL || px < P) sX[px * CINP + ct * 32 + l32] = (E)(acc[t][ct][i] + biasv[ct]);
+            if (FULL || px < P) sX[px * CINP + ct * 32 + l32] = (E)pin_f32(acc[t][ct][i] + biasv[ct]);
           }
       if (more) store_wtap<E, NWC>(sW, tid, wr);
       if (tid < COUT) {  // z = y * scale + shift (+ res), then ReLU, then * dropout scale
@@ -370,7 +370,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_fwd(TrunkFwdPar
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const float z = fmaxf(__builtin_fmaf((float)y8[j], ca[k % 3][j], cb[k % 3][j]) + (float)r8[j], 0.f);
-            o8[j] = (E)(z * cd[k % 3][j]);
+            o8[j] = (E)pin_f32(z * cd[k % 3][j]);
             mb |= ((float)o8[j] > 0.f ? 1u : 0u) << j;
           }
           const u32x4 ov = __builtin_bit_cast(u32x4, o8);
@@ -614,7 +614,7 @@ __global__ __launch_bounds__(512, 1) void k_trunk_fwd2(TrunkFwdParams<E> p) {
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const int px = (wave * NPT + t) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-            if (FULL || px < P) sX[px * CINP + ct * 32 + l32] = (E)(acc[t][ct][i] + biasv[ct]);
+            if (FULL || px < P) sX[px * CINP + ct * 32 + l32] = (E)pin_f32(acc[t][ct][i] + biasv[ct]);
           }
       if (more) store_wtap2<E>(sW0, wid, wr);  // buffer 0: last read by tap 8
       if (tid < COUT) {  // z = y * scale + shift (+ res), then ReLU, then * dropout scale
@@ -685,7 +685,7 @@ __global__ __launch_bounds__(512, 1) void k_trunk_fwd2(TrunkFwdParams<E> p) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const float z = fmaxf(__builtin_fmaf((float)y8[j], ca[k % 3][j], cb[k % 3][j]) + (float)r8[j], 0.f);
-            o8[j] = (E)(z * cd[k % 3][j]);
+            o8[j] = (E)pin_f32(z * cd[k % 3][j]);
             mb |= ((float)o8[j] > 0.f ? 1u : 0u) << j;
           }
           const u32x4 ov = __builtin_bit_cast(u32x4, o8);
@@ -850,7 +850,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_bwd(TrunkBwdPar
               if (addd) {  // + the skip gradient, rounded as the per-layer kernel's dx (+ addend) store
                 const E8 a8 = __builtin_bit_cast(E8, dv[u]);
 #pragma unroll
-                for (int j = 0; j < 8; ++j) d8[j] = (E)((float)d8[j] + (float)a8[j]);
+                for (int j = 0; j < 8; ++j) d8[j] = (E)pin_f32((float)d8[j] + (float)a8[j]);
               }
             }
             const E8 y8 = __builtin_bit_cast(E8, yr[i]);

@@ -82,6 +82,17 @@ int64_t mc_conv_gn_bwd_workspace(int32_t n, int32_t h, int32_t w_, int32_t cin);
 int mc_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* work, int64_t work_floats, int32_t n,
                   int32_t h, int32_t w_, int32_t cin, int32_t dtype, void* stream);
 
+/* mc_conv_wgrad of a 96-channel layer whose input x is the output of a previous layer's
+ * GroupNorm + ReLU (+ Dropout2d) without a residual -- a block's conv1 output, cnn_residual.py:
+ * 15-18 -- recomputed from that layer's saved y instead of read: x = 16-bit(max(y * a + b, 0) * d)
+ * with a = gamma * rstd, b = beta - mean * a per (sample, channel) from its stats [N][6][2] and
+ * affine parameters, d = dmask [N][96] (NULL: 1), rounded as the forward epilogue rounds, so dw
+ * is bitwise mc_conv_wgrad's on the saved x. The trunk forward then need not write x at all.
+ * 16x16 boards (k_wgrad_c96) only; MS_EINVAL otherwise. */
+int mc_conv_wgrad_gn(const uint16_t* dy, const uint16_t* y, const float* stats, const float* gamma, const float* beta,
+                     const float* dmask, float* dw, float* work, int64_t work_floats, int32_t n, int32_t h, int32_t w_,
+                     int32_t dtype, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * The whole residual stack in one launch per direction (csrc/mscnn_trunk.hip). Replaces,
  * for `blocks` residual blocks of 96 channels (cnn_residual.py:7-27, 55-56), the per-layer

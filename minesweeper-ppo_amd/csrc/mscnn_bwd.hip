@@ -370,6 +370,13 @@ struct WgradParams {
   float* part;  // [G][9][96][CIN]
   int N, H, W, G;
   int exp;  // MC_WSX builds: timing experiments (WGX_* bits; results wrong)
+  // x recomputed from a GroupNorm layer's saved y (k_wgrad_c96 only; gn_stats == null: x is x):
+  // x = 16-bit(max(y * a + b, 0) * d), a = gamma * rstd, b = beta - mean * a, d = dmask or 1,
+  // every step rounded as the forward epilogue that produced x rounds it (mc_conv_wgrad_gn)
+  const float* gn_stats;  // [N][6][2] (mean, rstd)
+  const float* gn_gamma;
+  const float* gn_beta;
+  const float* gn_dmask;  // [N][96] or null
 };
 // timing experiments of k_wgrad (libmsenv_wsx.so, mc_set_wgrad_exp; tools/wgrad_exp.py): each bit
 // removes one part so its cost can be read off the launch time
@@ -586,7 +593,8 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams<E> p) {
 // tiles per SIMD. Partials [G][9][96][96] as k_wgrad's, same k_reduce.
 constexpr int WC_DY = 256 * COUT;       // elements of one dy buffer
 constexpr int WC_SX = 18 * 18 * COUT;   // zero-halo x image, 96 channels a pixel
-constexpr int WC_LDS = (2 * WC_DY + WC_SX) * 2;  // 160,512 B
+constexpr int WC_CO = 3 * COUT;          // floats of the GroupNorm-apply coefficients (a | b | d)
+constexpr int WC_LDS = (2 * WC_DY + WC_SX) * 2 + WC_CO * 4;  // 160,512 + 1,152 B
 static_assert(WC_LDS <= 160 * 1024, "k_wgrad_c96 LDS");
 
 // One full-wave LDS-DMA of 1 KiB (16 B a lane, lane-linear at LDS byte address m0v) issued from
@@ -606,10 +614,21 @@ struct WgcTiles {
   static constexpr int cis(int bi) { return bi < 3 ? bi : M8; }
 };
 
-template <typename E, int WV>
-__device__ __forceinline__ void wgc_body(const WgradParams<E>& p, E* sDY, E* sX, int gid) {
+template <typename E, int WV, bool GN>
+__device__ __forceinline__ void wgc_body(const WgradParams<E>& p, E* sDY, E* sX, float* sCo, int gid) {
   typedef typename EV<E>::v8 E8;
   using T = WgcTiles<WV>;
+  // GN: waves 6 and 7 (threads 384 .. 479: channel c = tid - 384) fetch sample n's mean / rstd /
+  // dmask with its prefetch and write a | b | d to sCo after their MFMA loop; sCo is read by
+  // put_x after the barrier that frees sX (its previous reader, the last put_x, is a barrier back)
+  constexpr bool CO = GN && WV >= 6;
+  const int cc = threadIdx.x - 384;
+  const bool cact = CO && cc < COUT;
+  float cg = 0.f, cbt = 0.f, cm = 0.f, cr = 0.f, cdm = 1.f;
+  if (cact) {
+    cg = p.gn_gamma[cc];
+    cbt = p.gn_beta[cc];
+  }
   constexpr int NT = T::NT;
   const int tid = threadIdx.x, lane = tid & 63;
   const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
@@ -637,18 +656,55 @@ __device__ __forceinline__ void wgc_body(const WgradParams<E>& p, E* sDY, E* sX,
 #pragma unroll
         for (int k = 0; k < 6; ++k) rx[k] = xs[tid + 512 * k];
       }
+      if (cact) {
+        cm = p.gn_stats[((size_t)n * NGRP + (cc >> 4)) * 2];
+        cr = p.gn_stats[((size_t)n * NGRP + (cc >> 4)) * 2 + 1];
+        if (p.gn_dmask) cdm = p.gn_dmask[(size_t)n * COUT + cc];
+      }
+    }
+  };
+  auto put_co = [&]() {  // (the forward's coefficients, same operations: a, then b from a)
+#pragma clang fp contract(off)  // b = beta - (mean * a) rounded twice, as the forward computes it
+    if (cact) {
+      const float a = cg * cr;
+      sCo[cc] = a;
+      sCo[COUT + cc] = cbt - cm * a;
+      sCo[2 * COUT + cc] = cdm;
     }
   };
   auto put_x = [&]() {
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
       const int c = tid + 512 * k, px = c / 12, kk = c - px * 12;
-      *reinterpret_cast<u32x4*>(&sX[(((px >> 4) + 1) * 18 + (px & 15) + 1) * COUT + kk * 8]) = rx[k];
+      u32x4 v = rx[k];
+      if constexpr (GN) {  // the forward epilogue's z = max(y a + b + 0, 0), x = 16-bit(z d)
+#pragma clang fp contract(off)
+        const E8 y8 = __builtin_bit_cast(E8, v);
+        E8 o8;
+#pragma unroll
+        for (int h4 = 0; h4 < 2; ++h4) {
+          const f32x4 a4 = *reinterpret_cast<const f32x4*>(&sCo[kk * 8 + 4 * h4]);
+          const f32x4 b4 = *reinterpret_cast<const f32x4*>(&sCo[COUT + kk * 8 + 4 * h4]);
+          const f32x4 d4 = *reinterpret_cast<const f32x4*>(&sCo[2 * COUT + kk * 8 + 4 * h4]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int j = 4 * h4 + e;
+            const float z = fmaxf(__builtin_fmaf((float)y8[j], a4[e], b4[e]) + 0.0f, 0.f);
+            o8[j] = (E)pin_f32(z * d4[e]);
+          }
+        }
+        v = __builtin_bit_cast(u32x4, o8);
+      }
+      *reinterpret_cast<u32x4*>(&sX[(((px >> 4) + 1) * 18 + (px & 15) + 1) * COUT + kk * 8]) = v;
     }
   };
   int buf = 0;
   issue(gid, 0);
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (a builtin, so that the compiler's own count sees it)
+  if constexpr (GN) {
+    put_co();
+    __syncthreads();  // sCo complete
+  }
   put_x();
   __syncthreads();
   for (int n = gid; n < p.N; n += p.G, buf ^= 1) {
@@ -705,7 +761,10 @@ __device__ __forceinline__ void wgc_body(const WgradParams<E>& p, E* sDY, E* sX,
         __builtin_amdgcn_sched_group_barrier(0x008, NT, 0);
       }
     }
-    __syncthreads();  // sX and sDY[buf] are free
+    if constexpr (CO) {  // sample n + G's coefficients (its loads were issued with the prefetch)
+      if (n + p.G < p.N) put_co();
+    }
+    __syncthreads();  // sX and sDY[buf] are free; sCo holds sample n + G's coefficients
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMA and x loads have landed
     if (n + p.G < p.N && !WGX(WGX_NO_STAGE) && !WGX(WGX_NO_XLOAD)) put_x();
     __syncthreads();  // sX and sDY[buf ^ 1] (every wave's DMA) complete
@@ -721,23 +780,24 @@ __device__ __forceinline__ void wgc_body(const WgradParams<E>& p, E* sDY, E* sX,
   }
 }
 
-template <typename E>
+template <typename E, bool GN>
 __global__ __launch_bounds__(512, 1) void k_wgrad_c96(WgradParams<E> p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   E* sDY = reinterpret_cast<E*>(smem);  // [2][256][96]
   E* sX = sDY + 2 * WC_DY;              // [18 * 18][96], zero halo
+  float* sCo = reinterpret_cast<float*>(sX + WC_SX);  // [3][96] (GN)
   for (int i = threadIdx.x; i < WC_SX / 8; i += 512) *reinterpret_cast<u32x4*>(&sX[i * 8]) = u32x4{0u, 0u, 0u, 0u};
   __syncthreads();
   const int gid = blockIdx.x;
   switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-    case 0: wgc_body<E, 0>(p, sDY, sX, gid); break;
-    case 1: wgc_body<E, 1>(p, sDY, sX, gid); break;
-    case 2: wgc_body<E, 2>(p, sDY, sX, gid); break;
-    case 3: wgc_body<E, 3>(p, sDY, sX, gid); break;
-    case 4: wgc_body<E, 4>(p, sDY, sX, gid); break;
-    case 5: wgc_body<E, 5>(p, sDY, sX, gid); break;
-    case 6: wgc_body<E, 6>(p, sDY, sX, gid); break;
-    default: wgc_body<E, 7>(p, sDY, sX, gid); break;
+    case 0: wgc_body<E, 0, GN>(p, sDY, sX, sCo, gid); break;
+    case 1: wgc_body<E, 1, GN>(p, sDY, sX, sCo, gid); break;
+    case 2: wgc_body<E, 2, GN>(p, sDY, sX, sCo, gid); break;
+    case 3: wgc_body<E, 3, GN>(p, sDY, sX, sCo, gid); break;
+    case 4: wgc_body<E, 4, GN>(p, sDY, sX, sCo, gid); break;
+    case 5: wgc_body<E, 5, GN>(p, sDY, sX, sCo, gid); break;
+    case 6: wgc_body<E, 6, GN>(p, sDY, sX, sCo, gid); break;
+    default: wgc_body<E, 7, GN>(p, sDY, sX, sCo, gid); break;
   }
 }
 
@@ -877,12 +937,30 @@ int check_launch(const char* what) {
   return MS_OK;
 }
 
+struct GnApply {  // mc_conv_wgrad_gn: x recomputed from a layer's y (all null: x is given)
+  const float *stats = nullptr, *gamma = nullptr, *beta = nullptr, *dmask = nullptr;
+};
+
+template <typename E, bool GN>
+void launch_wgrad_c96(const WgradParams<E>& wp, int grid, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_wgrad_c96<E, GN>, hipFuncAttributeMaxDynamicSharedMemorySize, WC_LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL((k_wgrad_c96<E, GN>), dim3(grid), dim3(512), (size_t)WC_LDS, s, wp);
+}
+
 template <typename E>
 int run_wgrad(const Plan& pl, const uint16_t* dy, const uint16_t* x, float* dw, float* work, int32_t n, int32_t h,
-              int32_t w_, int32_t cin, hipStream_t s) {
+              int32_t w_, int32_t cin, hipStream_t s, const GnApply& gn = GnApply()) {
   WgradParams<E> wp;
   wp.dy = reinterpret_cast<const E*>(dy);
   wp.x = reinterpret_cast<const E*>(x);
+  wp.gn_stats = gn.stats;
+  wp.gn_gamma = gn.gamma;
+  wp.gn_beta = gn.beta;
+  wp.gn_dmask = gn.dmask;
   wp.part = work + pl.gn_part;
   wp.N = n;
   wp.H = h;
@@ -895,12 +973,8 @@ int run_wgrad(const Plan& pl, const uint16_t* dy, const uint16_t* x, float* dw, 
 #endif
   const size_t lds = (size_t)wgrad_lds(h, w_);
   if (pl.c96) {
-    static bool attr = false;
-    if (!attr) {
-      set_lds_attr(k_wgrad_c96<E>);
-      attr = true;
-    }
-    hipLaunchKernelGGL(k_wgrad_c96<E>, dim3(pl.grid_w), dim3(512), (size_t)WC_LDS, s, wp);
+    if (gn.stats) launch_wgrad_c96<E, true>(wp, pl.grid_w, s);
+    else launch_wgrad_c96<E, false>(wp, pl.grid_w, s);
   } else if (cin == 96) launch_wgrad<E, 96>(wp, pl.grid_w, lds, s);
   else launch_wgrad<E, 16>(wp, pl.grid_w, lds, s);
   int rc;
@@ -977,6 +1051,35 @@ int mc_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* work,
   if (dtype == MC_DT_BF16) return run_wgrad<__bf16>(pl, dy, x, dw, work, n, h, w_, cin, s);
   if (dtype == MC_DT_F16) return run_wgrad<_Float16>(pl, dy, x, dw, work, n, h, w_, cin, s);
   snprintf(g_err, sizeof g_err, "mc_conv_wgrad: dtype %d unsupported (0 bf16, 1 f16)", dtype);
+  return MS_EINVAL;
+}
+
+int mc_conv_wgrad_gn(const uint16_t* dy, const uint16_t* y, const float* stats, const float* gamma, const float* beta,
+                     const float* dmask, float* dw, float* work, int64_t work_floats, int32_t n, int32_t h, int32_t w_,
+                     int32_t dtype, void* stream) {
+  if (!dy || !y || !stats || !gamma || !beta || !dw || !work || n <= 0 || h <= 0 || w_ <= 0) {
+    snprintf(g_err, sizeof g_err, "mc_conv_wgrad_gn: bad argument");
+    return MS_EINVAL;
+  }
+  const Plan pl = make_plan(n, h, w_, 96);
+  if (!pl.c96) {
+    snprintf(g_err, sizeof g_err, "mc_conv_wgrad_gn: needs k_wgrad_c96 (16x16 boards, weight-gradient variant 0 or 3)");
+    return MS_EINVAL;
+  }
+  if (work_floats < pl.gn_part + pl.w_part) {
+    snprintf(g_err, sizeof g_err, "mc_conv_wgrad_gn: workspace %lld < %lld floats", (long long)work_floats,
+             (long long)(pl.gn_part + pl.w_part));
+    return MS_EINVAL;
+  }
+  GnApply gn;
+  gn.stats = stats;
+  gn.gamma = gamma;
+  gn.beta = beta;
+  gn.dmask = dmask;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MC_DT_BF16) return run_wgrad<__bf16>(pl, dy, y, dw, work, n, h, w_, 96, s, gn);
+  if (dtype == MC_DT_F16) return run_wgrad<_Float16>(pl, dy, y, dw, work, n, h, w_, 96, s, gn);
+  snprintf(g_err, sizeof g_err, "mc_conv_wgrad_gn: dtype %d unsupported (0 bf16, 1 f16)", dtype);
   return MS_EINVAL;
 }
 

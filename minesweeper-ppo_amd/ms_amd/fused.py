@@ -60,12 +60,21 @@ class kernel_variant:
         self.kernel, self.variant = kernel, variant
 
     def __enter__(self):
+        global _WGRAD_VARIANT
         _check(_fn("mc_set_variant", [_i32, _i32])(self.kernel, self.variant))
+        if self.kernel == VARIANT_WGRAD:
+            _WGRAD_VARIANT = self.variant
         return self
 
     def __exit__(self, *exc):
+        global _WGRAD_VARIANT
         _check(_fn("mc_set_variant", [_i32, _i32])(self.kernel, 0))
+        if self.kernel == VARIANT_WGRAD:
+            _WGRAD_VARIANT = 0
         return False
+
+
+_WGRAD_VARIANT = 0  # the weight-gradient variant kernel_variant set (0: the dispatcher's choice)
 
 
 def prep_weight(w: torch.Tensor, cin_pad: int, dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
@@ -279,11 +288,11 @@ class _BwdLayer(ctypes.Structure):  # mc_bwd_layer
     _fields_ = [(n, _vp) for n in ("ysave", "stats", "gamma", "relu_mask", "dmask", "wT", "dy")]
 
 
-_tf = _tfws = _tb = _tbws = _wg = None
+_tf = _tfws = _tb = _tbws = _wg = _wgn = None
 
 
 def _trunk_bind():
-    global _tf, _tfws, _tb, _tbws, _wg
+    global _tf, _tfws, _tb, _tbws, _wg, _wgn
     if _tf is None:
         _tf = _fn("mc_trunk_fwd", [_vp, ctypes.POINTER(_FwdLayer), _i32, _vp, ctypes.c_int64] + [_i32] * 3
                   + [_f32, _i32, _vp])
@@ -294,6 +303,7 @@ def _trunk_bind():
         _tbws = _fn("mc_trunk_bwd_workspace", [_i32] * 4)
         _tbws.restype = ctypes.c_int64
         _wg = _fn("mc_conv_wgrad", [_vp] * 4 + [ctypes.c_int64] + [_i32] * 5 + [_vp])
+        _wgn = _fn("mc_conv_wgrad_gn", [_vp] * 8 + [ctypes.c_int64] + [_i32] * 4 + [_vp])
 
 
 def chain_ok(layers, H: int, W: int) -> bool:
@@ -303,9 +313,17 @@ def chain_ok(layers, H: int, W: int) -> bool:
     return CHAIN and 0 < nres <= MAX_CHAIN_LAYERS and nres % 2 == 0 and H * W <= 512 and W <= 64
 
 
+def wgrad_gn_ok(H: int, W: int) -> bool:
+    """mc_conv_wgrad_gn's range: 16x16 boards under the default (or c96) weight gradient."""
+    return H == 16 and W == 16 and _WGRAD_VARIANT in (0, 3)
+
+
 def trunk_forward_chain(x, layers, H: int, W: int, dmasks, save: bool):
     """Residual stack (layers[1:]) on the stem output ``x`` [N, P, 96] in one mc_trunk_fwd.
-    Returns (out, outs, ys, sts, rms): per layer lists of the saved tensors (empty unless ``save``)."""
+    Returns (out, outs, ys, sts, rms): per layer lists of the saved tensors (empty unless ``save``).
+    Where mc_conv_wgrad_gn applies (``wgrad_gn_ok``), a block's conv1 output is not written: its
+    entry in ``outs`` is None and the backward recomputes it from the layer's y inside the weight
+    gradient."""
     _trunk_bind()
     n, p, c = x.shape
     assert c == COUT and x.is_contiguous() and p == H * W
@@ -325,7 +343,8 @@ def trunk_forward_chain(x, layers, H: int, W: int, dmasks, save: bool):
             dm = dmasks[k // 2].to(torch.float32).contiguous()
             assert dm.shape == (n, COUT)
         last = k == nl - 1
-        out = torch.empty((n, p, COUT), dtype=et, device=dev) if (save or last) else None
+        keep_out = save and not (k % 2 == 0 and wgrad_gn_ok(H, W))
+        out = torch.empty((n, p, COUT), dtype=et, device=dev) if (keep_out or last) else None
         y = torch.empty((n, p, COUT), dtype=et, device=dev) if save else None
         st = torch.empty((n, NGROUPS, 2), dtype=torch.float32, device=dev) if save else None
         rm = torch.empty((n, p, COUT // 8), dtype=torch.uint8, device=dev) if save else None
@@ -373,6 +392,29 @@ def trunk_backward_chain(dout, layers, ys, sts, rms, dmasks, H: int, W: int):
     work = torch.empty(nws, dtype=torch.uint8, device=dev)
     _check(_tb(L.ptr(dout), arr, nl, L.ptr(dgn), L.ptr(work), nws, n, H, W, _dt(dout), L.stream_ptr(dev)))
     return dys, dgn
+
+
+def conv_wgrad_gn(dy: torch.Tensor, y: torch.Tensor, stats: torch.Tensor, norm, dmask: Optional[torch.Tensor],
+                  H: int, W: int) -> torch.Tensor:
+    """conv_wgrad with x = the GroupNorm + ReLU (+ Dropout2d) output of the layer that saved ``y`` /
+    ``stats`` (``norm`` its GroupNorm, ``dmask`` [N, 96] or None), recomputed in the kernel
+    (mc_conv_wgrad_gn): bitwise conv_wgrad on the forward's x."""
+    _trunk_bind()
+    global _bwd_ws
+    if _bwd_ws is None:
+        _bwd_ws = _fn("mc_conv_gn_bwd_workspace", [_i32] * 4)
+        _bwd_ws.restype = ctypes.c_int64
+    n, p, c = y.shape
+    assert c == COUT and dy.shape == y.shape and dy.dtype == y.dtype and y.is_contiguous() and dy.is_contiguous()
+    g = norm.weight.detach().to(torch.float32).contiguous()
+    b = norm.bias.detach().to(torch.float32).contiguous()
+    dm = dmask.to(torch.float32).contiguous() if dmask is not None else None
+    dw = torch.empty((9, COUT, COUT), dtype=torch.float32, device=y.device)
+    nws = int(_bwd_ws(n, H, W, COUT))
+    work = torch.empty(nws, dtype=torch.float32, device=y.device)
+    _check(_wgn(L.ptr(dy), L.ptr(y), L.ptr(stats), L.ptr(g), L.ptr(b), L.ptr(dm), L.ptr(dw), L.ptr(work), nws, n, H, W,
+                _dt(y), L.stream_ptr(y.device)))
+    return dw
 
 
 def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, H: int, W: int) -> torch.Tensor:
@@ -452,7 +494,11 @@ class _TrunkFn(torch.autograd.Function):
             ctx.saved = None
             out = [None, None, None, None, None]
             for li, (conv, norm) in enumerate(layers):
-                dw = conv_wgrad(dys[li], acts[li], H, W)
+                if acts[li] is None:  # a block's conv1 output, not written by the forward
+                    dm = dmasks[(li - 2) // 2] if dmasks is not None else None
+                    dw = conv_wgrad_gn(dys[li], ys[li - 1], sts[li - 1], layers[li - 1][1], dm, H, W)
+                else:
+                    dw = conv_wgrad(dys[li], acts[li], H, W)
                 dys[li] = None
                 gs = (dw_to_conv(dw, conv.weight.shape[1]), dgn[li, 2], dgn[li, 0], dgn[li, 1])
                 for p, g in zip((conv.weight, conv.bias, norm.weight, norm.bias), gs):

@@ -97,6 +97,9 @@ def test_trunk_entry_points_validate_arguments():
     assert F._tfws(4, 40, 40) < 0 and F._tbws(3, 4, 40, 40) < 0  # boards of more than 512 cells
     assert F._wg(fake, fake, fake, fake, 1 << 30, 4, 16, 16, 32, 1, None) != 0  # cin 16 or 96 only
     assert b"mc_conv_wgrad" in lib.mc_last_error()
+    # mc_conv_wgrad_gn: y, stats, gamma, beta are required (dmask may be NULL)
+    assert F._wgn(fake, None, fake, fake, fake, None, fake, fake, 1 << 30, 4, 16, 16, 1, None) != 0
+    assert b"mc_conv_wgrad_gn: bad argument" in lib.mc_last_error()
 
 
 def test_set_variant_validates_each_kernel_range():

@@ -112,3 +112,25 @@ def test_trunk_chain_production_size(gpu, H, W, n):
     _assert_same(fa, fb, "features")
     for k in gb:
         _assert_same(ga[k], gb[k], k)
+
+
+@pytest.mark.parametrize("n,dmask", [(300, True), (1, False), (4100, True)])
+def test_wgrad_gn_equals_wgrad_on_saved_x(gpu, n, dmask):
+    """mc_conv_wgrad_gn (x recomputed from the producing layer's y, stats, GroupNorm affine and
+    dropout mask) is bitwise mc_conv_wgrad on the x the per-layer forward wrote, fp16 and bf16."""
+    from ms_amd import fused as F
+    H = W = 16
+    m = _model(1, gpu)
+    conv, norm = F.trunk_layers(m)[1]  # block 0's conv1: GroupNorm + ReLU + Dropout2d, no residual
+    for dt in (torch.float16, torch.bfloat16):
+        g = torch.Generator(device=gpu).manual_seed(11)
+        x0 = torch.randn((n, H * W, 96), device=gpu, generator=g).to(dt).contiguous()
+        dm = _dmasks(1, n, gpu)[0] if dmask else None
+        wt = F._packed(conv.weight, "f", dt, 96)
+        x, y, st, _ = F.conv_gn_fwd(x0, wt, conv.bias, norm.weight, norm.bias, H, W, dmask=dm, save=True,
+                                    eps=norm.eps, want_mask=True)
+        dy = torch.randn((n, H * W, 96), device=gpu, generator=g).to(dt).contiguous()
+        assert F.wgrad_gn_ok(H, W)
+        a = F.conv_wgrad_gn(dy, y, st, norm, dm, H, W)
+        b = F.conv_wgrad(dy, x, H, W)
+        _assert_same(a, b, f"dw {dt}")

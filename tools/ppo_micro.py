@@ -20,6 +20,7 @@ ap.add_argument("--amp", default="fp16")
 ap.add_argument("--fwd-only", action="store_true")
 ap.add_argument("--chain", type=int, default=1, help="one-launch trunk (1) or per-layer kernels (0)")
 ap.add_argument("--pure-bf16", action="store_true", help="model + obs in bf16, no autocast (timing only)")
+ap.add_argument("--torch-prof", type=int, default=0, help="print the device time of N minibatches by aten op")
 args = ap.parse_args()
 torch.backends.cudnn.benchmark = args.benchmark
 from ms_amd import fused as _F  # noqa: E402
@@ -81,3 +82,12 @@ dt = (time.perf_counter() - t0) / args.iters
 gf = (0.4388 if args.fwd_only else 1.3073) * M
 print(f"mb={M} cl={args.channels_last} bench={args.benchmark} amp={args.amp} fwd_only={args.fwd_only}: "
       f"{dt * 1e3:.1f} ms/iter, {gf / dt / 1e3:.1f} TFLOP/s, mem {torch.cuda.max_memory_allocated() / 1e9:.1f} GB")
+
+if args.torch_prof:
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+        for _ in range(args.torch_prof):
+            step()
+        torch.cuda.synchronize()
+    print(prof.key_averages(group_by_input_shape=True).table(sort_by="self_device_time_total", row_limit=60,
+                                                             max_name_column_width=40, max_shapes_column_width=70))

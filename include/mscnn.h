@@ -124,6 +124,13 @@ typedef struct mc_fwd_layer {
 int64_t mc_trunk_fwd_workspace(int32_t n, int32_t h, int32_t w_);
 int mc_trunk_fwd(const uint16_t* x0, const mc_fwd_layer* layers, int32_t nlayers, void* work, int64_t work_bytes,
                  int32_t n, int32_t h, int32_t w_, float eps, int32_t dtype, void* stream);
+/* mc_trunk_fwd that also writes pooled (f32 [N][96], NULL: not computed) = the last layer's
+ * output averaged over the P pixels (the value head's AdaptiveAvgPool2d(1), cnn_residual.py:
+ * 97-98), summed in f32 from the output tile while it is still on chip: no second pass over the
+ * features. */
+int mc_trunk_fwd_pooled(const uint16_t* x0, const mc_fwd_layer* layers, int32_t nlayers, void* work,
+                        int64_t work_bytes, float* pooled, int32_t n, int32_t h, int32_t w_, float eps, int32_t dtype,
+                        void* stream);
 
 /* Backward of the stem's GroupNorm + the residual stack: layers[0] = the stem (no input
  * gradient: wT NULL), layers[2b+1] / [2b+2] = conv1 / conv2 of block b (wT = the 16-bit

@@ -77,10 +77,36 @@ struct TrunkFwdParams {
   const E* x0;  // [N][P][96] block 0's input
   E* ws;        // [grid][P][96]: block outputs that are not kept (residual of the next block)
   unsigned long long* diag;  // MC_DIAG builds: per-wave phase cycle totals [grid][4][8]
+  float* pooled;  // [N][96] or null: the last layer's output averaged over the pixels
   int NL, N, H, W;
   float eps;
   TFLayer<E> L[MAXL];
 };
+
+// The value head's global average pool (cnn_residual.py:97-98, AdaptiveAvgPool2d(1)) of the
+// last layer's output tile while it is still in LDS: threads c + 96 h (h = 0, 1) sum channel c
+// over pixel half h on four interleaved f32 accumulators, the halves combine in fixed order
+// through sTmp ([2][96] f32), and the sum is scaled by 1 / P. Every thread of the workgroup
+// calls it (one barrier); out == null stores nothing.
+template <typename E>
+__device__ __forceinline__ void pool_tile(const E* sX, float* sTmp, int P, int tid, float* out) {
+  if (tid < 2 * COUT) {
+    const int c = tid % COUT, h = tid / COUT, half = (P + 1) >> 1;
+    const int p1 = h ? P : half;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int px = h ? half : 0;
+    for (; px + 3 < p1; px += 4) {
+      a0 += (float)sX[px * CINP + c];
+      a1 += (float)sX[(px + 1) * CINP + c];
+      a2 += (float)sX[(px + 2) * CINP + c];
+      a3 += (float)sX[(px + 3) * CINP + c];
+    }
+    for (; px < p1; ++px) a0 += (float)sX[px * CINP + c];
+    sTmp[h * COUT + c] = (a0 + a1) + (a2 + a3);
+  }
+  __syncthreads();
+  if (out && tid < COUT) out[tid] = (sTmp[tid] + sTmp[COUT + tid]) * (1.0f / (float)P);
+}
 
 __host__ __device__ inline int tf_region(int P) { return ((P + 1) * CINP + 7) & ~7; }
 __host__ __device__ inline size_t tf_lds(int P) {
@@ -382,6 +408,7 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_fwd(TrunkFwdPar
       __syncthreads();  // the tile and sAB are complete / free
       TSTAMP(4);
     }
+    if (p.pooled) pool_tile(sX, sAB, P, threadIdx.x, p.pooled + (size_t)n * COUT);  // (uniform)
   }
 #ifdef MC_DIAG
   if (p.diag && (threadIdx.x & 63) == 0)
@@ -697,6 +724,8 @@ __global__ __launch_bounds__(512, 1) void k_trunk_fwd2(TrunkFwdParams<E> p) {
       __syncthreads();  // the tile and sAB are complete / free
       TSTAMP(4);
     }
+    if (p.pooled)  // (uniform) the invalid team of an odd N stores nothing
+      pool_tile(sX, sAB, P, threadIdx.x & 255, valid ? p.pooled + (size_t)n * COUT : nullptr);
   }
 #ifdef MC_DIAG
   if (p.diag && (threadIdx.x & 63) == 0 && team == 0)
@@ -1144,11 +1173,12 @@ int launch_trunk_fwd2(const TrunkFwdParams<E>& p, hipStream_t s) {
 
 template <typename E>
 int run_trunk_fwd(const uint16_t* x0, const mc_fwd_layer* layers, int nl, void* work, int n, int h, int w,
-                  float eps, hipStream_t s) {
+                  float eps, float* pooled, hipStream_t s) {
   TrunkFwdParams<E> p;
   memset(&p, 0, sizeof p);
   p.x0 = reinterpret_cast<const E*>(x0);
   p.ws = reinterpret_cast<E*>(work);
+  p.pooled = pooled;
   p.NL = nl;
   p.N = n;
   p.H = h;
@@ -1267,6 +1297,12 @@ int64_t mc_trunk_fwd_workspace(int32_t n, int32_t h, int32_t w_) {
 
 int mc_trunk_fwd(const uint16_t* x0, const mc_fwd_layer* layers, int32_t nlayers, void* work, int64_t work_bytes,
                  int32_t n, int32_t h, int32_t w_, float eps, int32_t dtype, void* stream) {
+  return mc_trunk_fwd_pooled(x0, layers, nlayers, work, work_bytes, nullptr, n, h, w_, eps, dtype, stream);
+}
+
+int mc_trunk_fwd_pooled(const uint16_t* x0, const mc_fwd_layer* layers, int32_t nlayers, void* work,
+                        int64_t work_bytes, float* pooled, int32_t n, int32_t h, int32_t w_, float eps, int32_t dtype,
+                        void* stream) {
   if (!trunk_shape_ok(n, h, w_, nlayers, MAXL, "mc_trunk_fwd")) return MS_EINVAL;
   if (!x0 || !layers || (nlayers & 1)) {
     snprintf(g_err, sizeof g_err, "mc_trunk_fwd: bad argument (x0, layers, or an odd layer count %d)", nlayers);
@@ -1295,8 +1331,8 @@ int mc_trunk_fwd(const uint16_t* x0, const mc_fwd_layer* layers, int32_t nlayers
     return MS_EINVAL;
   }
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == MC_DT_BF16) return run_trunk_fwd<__bf16>(x0, layers, nlayers, work, n, h, w_, eps, s);
-  if (dtype == MC_DT_F16) return run_trunk_fwd<_Float16>(x0, layers, nlayers, work, n, h, w_, eps, s);
+  if (dtype == MC_DT_BF16) return run_trunk_fwd<__bf16>(x0, layers, nlayers, work, n, h, w_, eps, pooled, s);
+  if (dtype == MC_DT_F16) return run_trunk_fwd<_Float16>(x0, layers, nlayers, work, n, h, w_, eps, pooled, s);
   snprintf(g_err, sizeof g_err, "mc_trunk_fwd: dtype %d unsupported (0 bf16, 1 f16)", dtype);
   return MS_EINVAL;
 }

@@ -294,8 +294,8 @@ _tf = _tfws = _tb = _tbws = _wg = _wgn = None
 def _trunk_bind():
     global _tf, _tfws, _tb, _tbws, _wg, _wgn
     if _tf is None:
-        _tf = _fn("mc_trunk_fwd", [_vp, ctypes.POINTER(_FwdLayer), _i32, _vp, ctypes.c_int64] + [_i32] * 3
-                  + [_f32, _i32, _vp])
+        _tf = _fn("mc_trunk_fwd_pooled", [_vp, ctypes.POINTER(_FwdLayer), _i32, _vp, ctypes.c_int64, _vp]
+                  + [_i32] * 3 + [_f32, _i32, _vp])
         _tfws = _fn("mc_trunk_fwd_workspace", [_i32] * 3)
         _tfws.restype = ctypes.c_int64
         _tb = _fn("mc_trunk_bwd", [_vp, ctypes.POINTER(_BwdLayer), _i32, _vp, _vp, ctypes.c_int64] + [_i32] * 4
@@ -318,12 +318,12 @@ def wgrad_gn_ok(H: int, W: int) -> bool:
     return H == 16 and W == 16 and _WGRAD_VARIANT in (0, 3)
 
 
-def trunk_forward_chain(x, layers, H: int, W: int, dmasks, save: bool):
+def trunk_forward_chain(x, layers, H: int, W: int, dmasks, save: bool, pooled: Optional[torch.Tensor] = None):
     """Residual stack (layers[1:]) on the stem output ``x`` [N, P, 96] in one mc_trunk_fwd.
     Returns (out, outs, ys, sts, rms): per layer lists of the saved tensors (empty unless ``save``).
     Where mc_conv_wgrad_gn applies (``wgrad_gn_ok``), a block's conv1 output is not written: its
     entry in ``outs`` is None and the backward recomputes it from the layer's y inside the weight
-    gradient."""
+    gradient. ``pooled`` (f32 [N, 96]) receives the output's mean over the pixels."""
     _trunk_bind()
     n, p, c = x.shape
     assert c == COUT and x.is_contiguous() and p == H * W
@@ -360,8 +360,10 @@ def trunk_forward_chain(x, layers, H: int, W: int, dmasks, save: bool):
             final = out
     nws = int(_tfws(n, H, W))
     work = None if save else torch.empty(max(nws, 0), dtype=torch.uint8, device=dev)
-    _check(_tf(L.ptr(x), arr, nl, L.ptr(work), 0 if work is None else work.numel(), n, H, W, eps, _dt(x),
-               L.stream_ptr(dev)))
+    if pooled is not None:
+        assert pooled.shape == (n, COUT) and pooled.dtype == torch.float32 and pooled.is_contiguous()
+    _check(_tf(L.ptr(x), arr, nl, L.ptr(work), 0 if work is None else work.numel(), L.ptr(pooled), n, H, W, eps,
+               _dt(x), L.stream_ptr(dev)))
     return final, outs, ys, sts, rms
 
 
@@ -434,21 +436,30 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, H: int, W: int) -> torch.Tenso
     return dw
 
 
-def _trunk_forward(x0, layers, H, W, dmasks, save):
+def _trunk_forward(x0, layers, H, W, dmasks, save, pooled=None):
     """Runs every layer; with ``save`` returns the tensors the backward needs:
-    acts[l] = input of layer l (acts[l + 1] = its output), ys[l], sts[l], and the ReLU bitmasks."""
-    if chain_ok(layers, H, W):
-        conv, norm = layers[0]
-        wt = _packed(conv.weight, "f", x0.dtype, x0.shape[-1])
-        if save:
-            x, y, st, rm = conv_gn_fwd(x0, wt, conv.bias, norm.weight, norm.bias, H, W, save=True, eps=norm.eps,
-                                       want_mask=True)
-        else:
-            x, _, _ = conv_gn_fwd(x0, wt, conv.bias, norm.weight, norm.bias, H, W, save=False, eps=norm.eps)
-        out, outs, ys, sts, rms = trunk_forward_chain(x, layers, H, W, dmasks, save)
-        if not save:
-            return out, [], [], [], []
-        return out, [x0, x] + outs, [y] + ys, [st] + sts, [rm] + rms
+    acts[l] = input of layer l (acts[l + 1] = its output), ys[l], sts[l], and the ReLU bitmasks.
+    ``pooled`` (f32 [N, 96]): receives the output's mean over the pixels."""
+    if not chain_ok(layers, H, W):
+        x, acts, ys, sts, rms = _trunk_forward_layers(x0, layers, H, W, dmasks, save)
+        if pooled is not None:
+            pooled.copy_(x.mean(1, dtype=torch.float32))
+        return x, acts, ys, sts, rms
+    conv, norm = layers[0]
+    wt = _packed(conv.weight, "f", x0.dtype, x0.shape[-1])
+    if save:
+        x, y, st, rm = conv_gn_fwd(x0, wt, conv.bias, norm.weight, norm.bias, H, W, save=True, eps=norm.eps,
+                                   want_mask=True)
+    else:
+        x, _, _ = conv_gn_fwd(x0, wt, conv.bias, norm.weight, norm.bias, H, W, save=False, eps=norm.eps)
+    out, outs, ys, sts, rms = trunk_forward_chain(x, layers, H, W, dmasks, save, pooled=pooled)
+    if not save:
+        return out, [], [], [], []
+    return out, [x0, x] + outs, [y] + ys, [st] + sts, [rm] + rms
+
+
+def _trunk_forward_layers(x0, layers, H, W, dmasks, save):
+    """_trunk_forward through the per-layer kernels."""
     acts, ys, sts, rms = [x0], [], [], []
     x, blk_in = x0, None
     for li, (conv, norm) in enumerate(layers):
@@ -475,15 +486,19 @@ def _trunk_forward(x0, layers, H, W, dmasks, save):
 class _TrunkFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x0, H, W, dmasks, layers, *params):
+        """-> (features, pooled): pooled = the features' f32 mean over the pixels, an output
+        without a gradient of its own (the heads' backward adds its gradient to df)."""
         ctx.chain = chain_ok(layers, H, W)  # the backward takes the path the forward took
-        out, acts, ys, sts, rms = _trunk_forward(x0, layers, H, W, dmasks, save=True)
+        pooled = torch.empty((x0.shape[0], COUT), dtype=torch.float32, device=x0.device)
+        out, acts, ys, sts, rms = _trunk_forward(x0, layers, H, W, dmasks, save=True, pooled=pooled)
         ctx.H, ctx.W, ctx.layers, ctx.dmasks = H, W, layers, dmasks
         ctx.saved = (acts, ys, sts, rms)
         ctx.nparams = len(params)
-        return out
+        ctx.mark_non_differentiable(pooled)
+        return out, pooled
 
     @staticmethod
-    def backward(ctx, dout):
+    def backward(ctx, dout, _dpooled):
         acts, ys, sts, rms = ctx.saved
         layers, H, W, dmasks = ctx.layers, ctx.H, ctx.W, ctx.dmasks
         grads = {}
@@ -535,10 +550,13 @@ def trunk_params(layers) -> list:
 
 
 def fused_features(model, obs: torch.Tensor, dtype: torch.dtype = torch.bfloat16,
-                   dmasks: Optional[list] = None) -> torch.Tensor:
+                   dmasks: Optional[list] = None, with_pooled: bool = False):
     """Trunk features of CNNResidualPolicy as NHWC ``dtype`` [N, H*W, 96] via the fused kernels
     (``dtype``: the autocast type, bf16 or fp16). ``dmasks``: per-block Dropout2d masks [N, 96]
-    (keep / (1 - p), ms_amd.dropout); without them a training-mode model draws torch-RNG masks."""
+    (keep / (1 - p), ms_amd.dropout); without them a training-mode model draws torch-RNG masks.
+    ``with_pooled``: returns (features, their f32 mean over the pixels [N, 96]), the mean taken by
+    the trunk kernel from the last tile on chip (no gradient of its own: heads_apply routes the
+    value head's gradient into df)."""
     n, H, W = obs.shape[0], obs.shape[-2], obs.shape[-1]  # f32 obs [N, 10, H, W] or u8 codes [N, H, W]
     layers = trunk_layers(model)
     x0 = obs_to_nhwc(obs, 16, dtype)
@@ -551,9 +569,11 @@ def fused_features(model, obs: torch.Tensor, dtype: torch.dtype = torch.bfloat16
         dmasks = None
     params = trunk_params(layers)
     if torch.is_grad_enabled() and any(q.requires_grad for q in params):
-        return _TrunkFn.apply(x0, H, W, dmasks, layers, *params)
-    out, _, _, _, _ = _trunk_forward(x0, layers, H, W, dmasks, save=False)
-    return out
+        out, pooled = _TrunkFn.apply(x0, H, W, dmasks, layers, *params)
+        return (out, pooled) if with_pooled else out
+    pooled = torch.empty((n, COUT), dtype=torch.float32, device=obs.device) if with_pooled else None
+    out, _, _, _, _ = _trunk_forward(x0, layers, H, W, dmasks, save=False, pooled=pooled)
+    return (out, pooled) if with_pooled else out
 
 
 # ------------------------------------------------------------------------------------
@@ -612,9 +632,10 @@ class _HeadsFn(torch.autograd.Function):
     reads f.detach() (cnn_residual.py:94), so its gradient never reaches f."""
 
     @staticmethod
-    def forward(ctx, f, pol, mine, *params):
+    def forward(ctx, f, pol, mine, pre, *params):
         lp, lm = heads_forward(f, pol, mine)
-        pooled = f.mean(1, dtype=torch.float32)  # f32 accumulation, no f32 copy of f
+        # the trunk kernel's mean (``pre``), or f32 accumulation here (no f32 copy of f)
+        pooled = pre.clone() if pre is not None else f.mean(1, dtype=torch.float32)
         ctx.save_for_backward(f)
         ctx.pol, ctx.mine = pol, mine
         return lp, pooled, lm
@@ -640,7 +661,7 @@ class _HeadsFn(torch.autograd.Function):
         work = torch.empty(nws, device=dev)
         _check(_hb(L.ptr(f), L.ptr(dlp), L.ptr(dlm), L.ptr(w1), None, L.ptr(b1), L.ptr(w2), L.ptr(gadd), p,
                    L.ptr(df), L.ptr(dw1), L.ptr(db1), L.ptr(dw2), L.ptr(work), nws, M, _dt(f), L.stream_ptr(dev)))
-        grads = [df, None, None]
+        grads = [df, None, None, None]
         for h, i, dl in [(pol, 0, dlp)] + ([(mine, 1, dlm)] if mine is not None else []):
             sl = slice(i * COUT, (i + 1) * COUT)
             db2 = dl.sum() if dl is not None else torch.zeros((), device=dev)
@@ -649,12 +670,13 @@ class _HeadsFn(torch.autograd.Function):
         return tuple(grads)
 
 
-def heads_apply(f: torch.Tensor, pol, mine=None):
-    """Policy logits f32 [N, P], pooled trunk features f32 [N, 96], mine logits [N, P] | None."""
+def heads_apply(f: torch.Tensor, pol, mine=None, pooled: Optional[torch.Tensor] = None):
+    """Policy logits f32 [N, P], pooled trunk features f32 [N, 96], mine logits [N, P] | None.
+    ``pooled``: f's mean over the pixels when the trunk already took it (fused_features)."""
     params = []
     for h in [pol] + ([mine] if mine is not None else []):
         params += [h[0].weight, h[0].bias, h[2].weight, h[2].bias]
     if torch.is_grad_enabled() and (f.requires_grad or any(q.requires_grad for q in params)):
-        return _HeadsFn.apply(f, pol, mine, *params)
+        return _HeadsFn.apply(f, pol, mine, pooled, *params)
     lp, lm = heads_forward(f, pol, mine)
-    return lp, f.mean(1, dtype=torch.float32), lm
+    return lp, (pooled if pooled is not None else f.mean(1, dtype=torch.float32)), lm

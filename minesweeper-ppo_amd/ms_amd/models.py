@@ -140,11 +140,12 @@ class CNNResidualPolicy(nn.Module):
             f = blk(f, dmasks[i] if dmasks is not None else None)
         return f
 
-    def _heads_fused(self, f: torch.Tensor, H: int, W: int, return_mine: bool):
-        """Heads through csrc/msheads.hip: policy + mine logits and the pooled features in
-        one pass over f; the value MLP (N x 96 -> 1) stays a PyTorch op."""
+    def _heads_fused(self, f: torch.Tensor, H: int, W: int, return_mine: bool, pooled=None):
+        """Heads through csrc/msheads.hip: policy + mine logits in one pass over f; the pooled
+        features come from the trunk kernel (``pooled``); the value MLP (N x 96 -> 1) stays a
+        PyTorch op."""
         from .fused import heads_apply
-        logits, pooled, mine = heads_apply(f, self.policy_head, self.mine_head if return_mine else None)
+        logits, pooled, mine = heads_apply(f, self.policy_head, self.mine_head if return_mine else None, pooled)
         vh = self.value_head
         value = vh[6](F.relu(vh[4](F.relu(vh[2](pooled))))).squeeze(-1)
         if return_mine:
@@ -157,8 +158,8 @@ class CNNResidualPolicy(nn.Module):
         dmasks = self.keyed_masks(x.shape[0])
         if self.use_fused(x):
             from .fused import fused_features
-            f = fused_features(self, x, torch.get_autocast_dtype("cuda"), dmasks=dmasks)
-            return self._heads_fused(f, x.shape[-2], x.shape[-1], return_mine)
+            f, pooled = fused_features(self, x, torch.get_autocast_dtype("cuda"), dmasks=dmasks, with_pooled=True)
+            return self._heads_fused(f, x.shape[-2], x.shape[-1], return_mine, pooled)
         if x.dtype == torch.uint8:
             from .fused import codes_to_obs
             x = codes_to_obs(x)

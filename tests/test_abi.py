@@ -78,16 +78,16 @@ def test_trunk_entry_points_validate_arguments():
     F._trunk_bind()
     fake = ctypes.c_void_p(4096)
     arr = (F._FwdLayer * 2)()
-    assert F._tf(fake, arr, 1, None, 0, 4, 16, 16, 1e-5, 1, None) != 0  # odd layer count
-    assert F._tf(fake, arr, 2, None, 0, 4, 16, 16, 1e-5, 1, None) != 0  # layer 0 has no weights
+    assert F._tf(fake, arr, 1, None, 0, None, 4, 16, 16, 1e-5, 1, None) != 0  # odd layer count
+    assert F._tf(fake, arr, 2, None, 0, None, 4, 16, 16, 1e-5, 1, None) != 0  # layer 0 has no weights
     assert b"layer 0" in lib.mc_last_error()
     for k in range(2):
         arr[k] = F._FwdLayer(4096, 4096, 4096, 4096, None, None, None, None, None)
-    assert F._tf(fake, arr, 2, None, 0, 4, 16, 16, 1e-5, 1, None) != 0  # the last layer's out is required
+    assert F._tf(fake, arr, 2, None, 0, None, 4, 16, 16, 1e-5, 1, None) != 0  # the last layer's out is required
     assert b"last layer" in lib.mc_last_error()
     arr[1] = F._FwdLayer(4096, 4096, 4096, 4096, 4096, 4096, None, None, None)
-    assert F._tf(fake, arr, 2, None, 0, 4, 16, 16, 1e-5, 1, None) != 0  # dropout on a conv2
-    assert F._tf(fake, arr, 17, None, 0, 4, 16, 16, 1e-5, 1, None) != 0  # > MC_TRUNK_MAX_LAYERS
+    assert F._tf(fake, arr, 2, None, 0, None, 4, 16, 16, 1e-5, 1, None) != 0  # dropout on a conv2
+    assert F._tf(fake, arr, 17, None, 0, None, 4, 16, 16, 1e-5, 1, None) != 0  # > MC_TRUNK_MAX_LAYERS
     barr = (F._BwdLayer * 3)()
     assert F._tb(fake, barr, 2, fake, fake, 1 << 30, 4, 16, 16, 1, None) != 0  # even layer count
     assert F._tb(fake, barr, 3, fake, fake, 1 << 30, 4, 16, 16, 1, None) != 0  # empty layers

@@ -134,3 +134,19 @@ def test_wgrad_gn_equals_wgrad_on_saved_x(gpu, n, dmask):
         a = F.conv_wgrad_gn(dy, y, st, norm, dm, H, W)
         b = F.conv_wgrad(dy, x, H, W)
         _assert_same(a, b, f"dw {dt}")
+
+
+@pytest.mark.parametrize("H,W,n,grad", [(16, 16, 300, True), (16, 16, 301, False), (9, 9, 203, True),
+                                        (9, 9, 131, False), (30, 16, 40, True), (5, 7, 17, False)])
+def test_trunk_pooled_equals_mean(gpu, H, W, n, grad):
+    """The value head's global average pool taken by the trunk kernel from the last tile on chip
+    (mc_trunk_fwd_pooled; k_trunk_fwd with saves, k_trunk_fwd2 without, odd N) equals the f32
+    mean of the features it wrote, within f32 summation-order rounding."""
+    from ms_amd import fused as F
+    m = _model(2, gpu)
+    obs = _obs(n, H, W, gpu)
+    with torch.set_grad_enabled(grad):
+        f, pooled = F.fused_features(m, obs, torch.float16, dmasks=_dmasks(2, n, gpu), with_pooled=True)
+    ref = f.detach().mean(1, dtype=torch.float32)
+    assert pooled.shape == (n, 96) and pooled.dtype == torch.float32
+    torch.testing.assert_close(pooled, ref, rtol=1e-5, atol=1e-5)

@@ -59,6 +59,10 @@ def f32_fwd():
         mlp(x0)
 
 
-for name, fn in [("fp16 autocast fwd+bwd", amp16), ("fp32 fwd+bwd", f32), ("bf16 autocast fwd+bwd", amp_bf16),
-                 ("fp16 autocast fwd (no grad)", amp16_fwd), ("fp32 fwd (no grad)", f32_fwd)]:
-    run(name, fn)
+for lib in ["default", "cublas", "cublaslt"]:
+    if lib != "default":
+        torch.backends.cuda.preferred_blas_library(lib)
+    print("blas:", torch.backends.cuda.preferred_blas_library())
+    for name, fn in [("fp16 autocast fwd+bwd", amp16), ("fp32 fwd+bwd", f32), ("bf16 autocast fwd+bwd", amp_bf16),
+                     ("fp16 autocast fwd (no grad)", amp16_fwd), ("fp32 fwd (no grad)", f32_fwd)]:
+        run(name, fn)

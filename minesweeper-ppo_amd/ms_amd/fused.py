@@ -313,9 +313,12 @@ def chain_ok(layers, H: int, W: int) -> bool:
     return CHAIN and 0 < nres <= MAX_CHAIN_LAYERS and nres % 2 == 0 and H * W <= 512 and W <= 64
 
 
+WGRAD_GN = True  # False: the forward writes every conv1 output and mc_conv_wgrad reads it (A/B timing)
+
+
 def wgrad_gn_ok(H: int, W: int) -> bool:
     """mc_conv_wgrad_gn's range: 16x16 boards under the default (or c96) weight gradient."""
-    return H == 16 and W == 16 and _WGRAD_VARIANT in (0, 3)
+    return WGRAD_GN and H == 16 and W == 16 and _WGRAD_VARIANT in (0, 3)
 
 
 def trunk_forward_chain(x, layers, H: int, W: int, dmasks, save: bool, pooled: Optional[torch.Tensor] = None):

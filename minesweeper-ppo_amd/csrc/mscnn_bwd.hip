@@ -673,29 +673,42 @@ __device__ __forceinline__ void wgc_body(const WgradParams<E>& p, E* sDY, E* sX,
     }
   };
   auto put_x = [&]() {
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      const int c = tid + 512 * k, px = c / 12, kk = c - px * 12;
-      u32x4 v = rx[k];
-      if constexpr (GN) {  // the forward epilogue's z = max(y a + b + 0, 0), x = 16-bit(z d)
+    if constexpr (GN) {
+      // chunks k and k + 3 of a thread hold the same 8 channels (512 = 42 * 12 + 8, so chunk k's
+      // channel group is (tid + 8k) mod 12): one read of their coefficients serves both. The
+      // forward epilogue's z = max(y a + b + 0, 0), x = 16-bit(z d); the "+ 0" only turns a -0 into
+      // +0, which the max and the weight gradient's sums cannot tell apart, so it is left out
 #pragma clang fp contract(off)
-        const E8 y8 = __builtin_bit_cast(E8, v);
-        E8 o8;
+#pragma unroll
+      for (int j3 = 0; j3 < 3; ++j3) {
+        const int kk = (tid + 512 * j3) % 12;
+        f32x4 a4[2], b4[2], d4[2];
 #pragma unroll
         for (int h4 = 0; h4 < 2; ++h4) {
-          const f32x4 a4 = *reinterpret_cast<const f32x4*>(&sCo[kk * 8 + 4 * h4]);
-          const f32x4 b4 = *reinterpret_cast<const f32x4*>(&sCo[COUT + kk * 8 + 4 * h4]);
-          const f32x4 d4 = *reinterpret_cast<const f32x4*>(&sCo[2 * COUT + kk * 8 + 4 * h4]);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int j = 4 * h4 + e;
-            const float z = fmaxf(__builtin_fmaf((float)y8[j], a4[e], b4[e]) + 0.0f, 0.f);
-            o8[j] = (E)pin_f32(z * d4[e]);
-          }
+          a4[h4] = *reinterpret_cast<const f32x4*>(&sCo[kk * 8 + 4 * h4]);
+          b4[h4] = *reinterpret_cast<const f32x4*>(&sCo[COUT + kk * 8 + 4 * h4]);
+          d4[h4] = *reinterpret_cast<const f32x4*>(&sCo[2 * COUT + kk * 8 + 4 * h4]);
         }
-        v = __builtin_bit_cast(u32x4, o8);
+#pragma unroll
+        for (int k = j3; k < 6; k += 3) {
+          const int c = tid + 512 * k, px = c / 12;
+          const E8 y8 = __builtin_bit_cast(E8, rx[k]);
+          E8 o8;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float z = fmaxf(__builtin_fmaf((float)y8[j], a4[j >> 2][j & 3], b4[j >> 2][j & 3]), 0.f);
+            o8[j] = (E)pin_f32(z * d4[j >> 2][j & 3]);
+          }
+          *reinterpret_cast<u32x4*>(&sX[(((px >> 4) + 1) * 18 + (px & 15) + 1) * COUT + kk * 8]) =
+              __builtin_bit_cast(u32x4, o8);
+        }
       }
-      *reinterpret_cast<u32x4*>(&sX[(((px >> 4) + 1) * 18 + (px & 15) + 1) * COUT + kk * 8]) = v;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const int c = tid + 512 * k, px = c / 12, kk = c - px * 12;
+        *reinterpret_cast<u32x4*>(&sX[(((px >> 4) + 1) * 18 + (px & 15) + 1) * COUT + kk * 8]) = rx[k];
+      }
     }
   };
   int buf = 0;

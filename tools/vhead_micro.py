@@ -66,3 +66,32 @@ for lib in ["default", "cublas", "cublaslt"]:
     for name, fn in [("fp16 autocast fwd+bwd", amp16), ("fp32 fwd+bwd", f32), ("bf16 autocast fwd+bwd", amp_bf16),
                      ("fp16 autocast fwd (no grad)", amp16_fwd), ("fp32 fwd (no grad)", f32_fwd)]:
         run(name, fn)
+
+
+# hand-written forward / backward (16-bit GEMMs forward and for the data gradients, f32
+# split-K batched GEMMs for the weight gradients)
+S = 32
+W16 = [m.weight.detach().half() for m in lin]
+B16 = [m.bias.detach().half() for m in lin]
+
+
+def manual():
+    x = x0.half()
+    a1 = torch.addmm(B16[0], x, W16[0].t())
+    h1 = torch.relu(a1)
+    a2 = torch.addmm(B16[1], h1, W16[1].t())
+    h2 = torch.relu(a2)
+    v = torch.addmm(B16[2], h2, W16[2].t())
+    dv = torch.ones_like(v)  # d(sum)/dv
+    dh2 = (dv * W16[2]) * (a2 > 0)
+    dw3 = (dv.float() * h2.float()).sum(0)
+    dh1 = (dh2 @ W16[1]) * (a1 > 0)
+    n = x.shape[0]
+    dw2 = torch.bmm(dh2.float().view(S, n // S, -1).transpose(1, 2), h1.float().view(S, n // S, -1)).sum(0)
+    dw1 = torch.bmm(dh1.float().view(S, n // S, -1).transpose(1, 2), x.float().view(S, n // S, -1)).sum(0)
+    dx = dh1 @ W16[0]
+    return dw1, dw2, dw3, dh2.float().sum(0), dh1.float().sum(0), dx
+
+
+torch.backends.cuda.preferred_blas_library("cublaslt")
+run("manual fwd+bwd (split-K f32 weight grads)", manual)

@@ -683,3 +683,61 @@ def heads_apply(f: torch.Tensor, pol, mine=None, pooled: Optional[torch.Tensor] 
         return _HeadsFn.apply(f, pol, mine, pooled, *params)
     lp, lm = heads_forward(f, pol, mine)
     return lp, (pooled if pooled is not None else f.mean(1, dtype=torch.float32)), lm
+
+
+# ------------------------------------------------------------------------------------
+# The value head's MLP (cnn_residual.py:97-102: Linear 96 -> H, ReLU, Linear H -> H, ReLU,
+# Linear H -> 1) on the pooled features under 16-bit autocast.
+
+VALUE_SPLITK = 32  # row chunks of the weight gradients' batched GEMMs; 0: autocast's nn.Linear chain
+
+
+class _ValueMLP(torch.autograd.Function):
+    """Forward exactly as autocast runs the three nn.Linear (16-bit addmm with 16-bit bias, ReLU
+    in 16 bits). Backward: the data gradients as autocast's (16-bit GEMMs), the weight gradients
+    as f32 split-K batched GEMMs over row chunks plus a fixed-order sum -- hipBLASLt runs the
+    K = N (32,768 rows) weight-gradient GEMMs at ~115 us each (tools/vhead_micro.py: 0.39 vs
+    0.55-0.63 ms a minibatch); they are f32 sums of the same 16-bit products, so they differ from
+    autocast's 16-bit-rounded weight gradients by at most that rounding."""
+
+    @staticmethod
+    def forward(ctx, pooled, dt, w1, b1, w2, b2, w3, b3):
+        x = pooled.to(dt)
+        W = [w.detach().to(dt) for w in (w1, w2, w3)]
+        a1 = torch.addmm(b1.detach().to(dt), x, W[0].t())
+        h1 = torch.relu(a1)
+        a2 = torch.addmm(b2.detach().to(dt), h1, W[1].t())
+        h2 = torch.relu(a2)
+        v = torch.addmm(b3.detach().to(dt), h2, W[2].t())
+        ctx.save_for_backward(x, h1, h2, *W)
+        return v
+
+    @staticmethod
+    def backward(ctx, dv):
+        x, h1, h2, W1, W2, W3 = ctx.saved_tensors
+        dv = dv.to(x.dtype)
+        n = x.shape[0]
+        s = VALUE_SPLITK if n % VALUE_SPLITK == 0 and n >= 64 * VALUE_SPLITK else 1
+
+        def wgrad(d, a):  # d^T a in f32, summed over s row chunks in order
+            d32, a32 = d.float(), a.float()
+            if s == 1:
+                return d32.t() @ a32
+            return torch.bmm(d32.view(s, n // s, -1).transpose(1, 2), a32.view(s, n // s, -1)).sum(0)
+
+        dh2 = (dv @ W3) * (h2 > 0)
+        dh1 = (dh2 @ W2) * (h1 > 0)
+        dx = (dh1 @ W1).float()
+        return (dx, None, wgrad(dh1, x), dh1.float().sum(0), wgrad(dh2, h1), dh2.float().sum(0),
+                wgrad(dv, h2), dv.float().sum(0))
+
+
+def value_mlp(vh, pooled: torch.Tensor) -> torch.Tensor:
+    """value [N] of the value head ``vh`` (nn.Sequential pool, flatten, Linear, ReLU, Linear,
+    ReLU, Linear) on ``pooled`` f32 [N, 96], under the active 16-bit autocast."""
+    l1, l2, l3 = vh[2], vh[4], vh[6]
+    dt = torch.get_autocast_dtype("cuda")
+    params = (l1.weight, l1.bias, l2.weight, l2.bias, l3.weight, l3.bias)
+    if VALUE_SPLITK and torch.is_grad_enabled() and (pooled.requires_grad or any(p.requires_grad for p in params)):
+        return _ValueMLP.apply(pooled, dt, *params).squeeze(-1)
+    return l3(torch.relu(l2(torch.relu(l1(pooled))))).squeeze(-1)

@@ -142,12 +142,11 @@ class CNNResidualPolicy(nn.Module):
 
     def _heads_fused(self, f: torch.Tensor, H: int, W: int, return_mine: bool, pooled=None):
         """Heads through csrc/msheads.hip: policy + mine logits in one pass over f; the pooled
-        features come from the trunk kernel (``pooled``); the value MLP (N x 96 -> 1) stays a
-        PyTorch op."""
-        from .fused import heads_apply
+        features come from the trunk kernel (``pooled``); the value MLP (N x 96 -> 1) is
+        PyTorch GEMMs with split-K weight gradients (fused.value_mlp)."""
+        from .fused import heads_apply, value_mlp
         logits, pooled, mine = heads_apply(f, self.policy_head, self.mine_head if return_mine else None, pooled)
-        vh = self.value_head
-        value = vh[6](F.relu(vh[4](F.relu(vh[2](pooled))))).squeeze(-1)
+        value = value_mlp(self.value_head, pooled)
         if return_mine:
             return logits, value, mine.view(f.shape[0], 1, H, W)
         return logits, value

@@ -250,3 +250,29 @@ def test_heads_bwd_deterministic(gpu, n, P):
         outs.append([f.grad.clone()] + [p.grad.clone() for p in list(pol.parameters()) + list(mine.parameters())])
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("n,dt", [(32768, torch.float16), (4100, torch.bfloat16), (64, torch.float16)])
+def test_value_mlp_matches_autocast(gpu, n, dt):
+    """fused.value_mlp (the value head's MLP with f32 split-K weight gradients): the forward is
+    autocast's nn.Linear chain bitwise; the gradients match autocast's within its 16-bit
+    rounding of the weight gradients (rel 2e-2 of the largest entry)."""
+    from ms_amd import fused as F
+    from ms_amd.models import CNNResidualPolicy
+    torch.manual_seed(0)
+    vh = CNNResidualPolicy(10, stem_channels=96, blocks=1, value_hidden=256).to(gpu).value_head
+    g = torch.Generator(device=gpu).manual_seed(5)
+    x = torch.randn(n, 96, device=gpu, generator=g)
+    dv = torch.randn(n, device=gpu, generator=g)
+    out = {}
+    for mode in ("fused", "autocast"):
+        vh.zero_grad(set_to_none=True)
+        xi = x.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=dt):
+            v = F.value_mlp(vh, xi) if mode == "fused" else vh[6](torch.relu(vh[4](torch.relu(vh[2](xi))))).squeeze(-1)
+        (v.float() * dv).sum().backward()
+        out[mode] = (v.detach(), xi.grad.clone(), [p.grad.clone() for p in vh.parameters()])
+    assert torch.equal(out["fused"][0], out["autocast"][0])
+    for a, b in zip([out["fused"][1]] + out["fused"][2], [out["autocast"][1]] + out["autocast"][2]):
+        assert a.shape == b.shape and a.dtype == b.dtype
+        assert (a - b).abs().max().item() <= 2e-2 * b.abs().max().item() + 1e-6

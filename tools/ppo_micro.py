@@ -21,6 +21,7 @@ ap.add_argument("--fwd-only", action="store_true")
 ap.add_argument("--chain", type=int, default=1, help="one-launch trunk (1) or per-layer kernels (0)")
 ap.add_argument("--pure-bf16", action="store_true", help="model + obs in bf16, no autocast (timing only)")
 ap.add_argument("--no-wgrad-gn", action="store_true", help="write conv1 outputs instead of recomputing them")
+ap.add_argument("--value-splitk", type=int, default=32, help="fused.VALUE_SPLITK (0: autocast's Linear chain)")
 ap.add_argument("--torch-prof", type=int, default=0, help="print the device time of N minibatches by aten op")
 args = ap.parse_args()
 torch.backends.cudnn.benchmark = args.benchmark
@@ -28,6 +29,7 @@ from ms_amd import fused as _F  # noqa: E402
 from ms_amd.models import build_model  # noqa: E402
 _F.CHAIN = bool(args.chain)
 _F.WGRAD_GN = not args.no_wgrad_gn
+_F.VALUE_SPLITK = args.value_splitk
 from ms_amd.ppo import PPOConfig, ppo_update  # noqa: E402
 from ms_amd.buffers import Batch  # noqa: E402
 

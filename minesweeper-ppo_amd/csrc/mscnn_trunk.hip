@@ -1201,10 +1201,10 @@ int run_trunk_fwd(const uint16_t* x0, const mc_fwd_layer* layers, int nl, void* 
   }
   const int P = h * w;
   // same-box A/B (profiles/r05/trunk_fwd2_ab.txt): the two-sample kernel is 3 % faster on the
-  // no-grad forward at 16x16 and 2-6 % at 9x9, but level with the saving forward at 16x16, whose
-  // store-heavy epilogues it runs in lockstep; the saving forward at 16x16 keeps k_trunk_fwd
-  const bool save = layers[0].ysave != nullptr;
-  if (fwd_two(P) && (!save || P <= 128)) {
+  // no-grad forward at 16x16 and 2-6 % at 9x9; on the saving forward at 16x16 it was level while
+  // every conv1 output was stored, and is 0.4 ms a minibatch faster since they are recomputed in
+  // the weight gradient instead (profiles/r05/trunk_fwd2_save_ab.txt)
+  if (fwd_two(P)) {
     if (P == 256) return launch_trunk_fwd2<E, 2, true>(p, s);
     return P <= 128 ? launch_trunk_fwd2<E, 1, false>(p, s) : launch_trunk_fwd2<E, 2, false>(p, s);
   }

@@ -97,8 +97,12 @@ int mc_conv_wgrad_gn(const uint16_t* dy, const uint16_t* y, const float* stats, 
  * The whole residual stack in one launch per direction (csrc/mscnn_trunk.hip). Replaces,
  * for `blocks` residual blocks of 96 channels (cnn_residual.py:7-27, 55-56), the per-layer
  * launches above: a sample's activations stay in the workgroup's LDS from layer to layer,
- * and only what the backward or the caller needs is written to HBM. Outputs are bitwise
- * those of the per-layer entry points on the same inputs. Boards of at most 512 cells.
+ * and only what the backward or the caller needs is written to HBM. Boards of at most 512
+ * cells. Outputs are bitwise those of the per-layer entry points on the same inputs, except the
+ * forward without saves (ysave / stats / relu_mask all NULL: the rollout's) on boards of <= 256
+ * cells, which runs the ping-pong kernel k_trunk_fwd_pp: the conv bias and the GroupNorm sums
+ * are accumulated in another f32 order, so its outputs agree to 16-bit rounding
+ * (tests/test_trunk_gpu.py PP_TOL).
  *
  * Forward: layers[0 .. 2*blocks-1] in execution order (conv1, conv2 of block 0, ...); x0
  * (16-bit [N][P][96]) is block 0's input. Per layer (host array of device pointers):

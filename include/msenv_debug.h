@@ -31,11 +31,15 @@ int ms_set_debug_flags(ms_handle* h, uint32_t flags);
  * Kernel 2 = the weight gradient on 16x16 boards with 96 channels: variant 0 = default (= 3),
  * 1 = k_wgrad (three ci-slice workgroups a sample group, the compiler's LDS-read schedule),
  * 2 = k_wgrad with the next step's reads pinned between this step's MFMAs, 3 = k_wgrad_c96 (one
- * workgroup a CU owns all 81 tiles; dy by LDS-DMA). Any other (kernel, variant) is MS_EINVAL.
- * Process-wide, not thread-safe. */
+ * workgroup a CU owns all 81 tiles; dy by LDS-DMA). Kernel 3 = mc_trunk_fwd on boards of <= 256
+ * cells: variant 0 = default (k_trunk_fwd_pp, the ping-pong forward, when nothing is saved --
+ * the rollout's forward; k_trunk_fwd2 when y / stats / ReLU bits are saved -- the training
+ * forward), 1 = k_trunk_fwd2 always, 2 = k_trunk_fwd_pp always. Any other (kernel, variant) is
+ * MS_EINVAL. Process-wide, not thread-safe. */
 #define MC_VAR_FWD 0
 #define MC_VAR_BWD 1
 #define MC_VAR_WGRAD 2
+#define MC_VAR_TRUNK_FWD 3
 int mc_set_variant(int32_t kernel, int32_t variant);
 
 /* Measurement (bench.py): while set, every k_step / k_run launch of this handle is

@@ -30,7 +30,7 @@
 namespace mc {
 
 thread_local char g_err[256] = "";
-int g_variant[MCV_COUNT] = {0, 0, 0};
+int g_variant[MCV_COUNT] = {0, 0, 0, 0};
 
 int num_cus() {
   static int ncu = 0;
@@ -530,7 +530,7 @@ extern "C" {
 const char* mc_last_error(void) { return g_err; }
 
 int mc_set_variant(int32_t kernel, int32_t variant) {
-  static const int vmax[MCV_COUNT] = {1, 1, 3};  // fwd, data backward, weight gradient
+  static const int vmax[MCV_COUNT] = {1, 1, 3, 2};  // fwd, data backward, weight gradient, trunk fwd
   if (kernel < 0 || kernel >= MCV_COUNT || variant < 0 || variant > vmax[kernel]) {
     snprintf(g_err, sizeof g_err, "mc_set_variant: bad kernel %d / variant %d", kernel, variant);
     return MS_EINVAL;

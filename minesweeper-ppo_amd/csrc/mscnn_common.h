@@ -119,7 +119,7 @@ __device__ __forceinline__ void grp_bar(unsigned* cnt, unsigned target, int lane
 }
 
 // Kernel variants (msenv_debug.h mc_set_variant): 0 = the dispatcher's choice.
-enum { MCV_FWD = 0, MCV_BWD = 1, MCV_WGRAD = 2, MCV_COUNT = 3 };
+enum { MCV_FWD = 0, MCV_BWD = 1, MCV_WGRAD = 2, MCV_TRUNK_FWD = 3, MCV_COUNT = 4 };
 extern int g_variant[MCV_COUNT];
 
 __device__ __forceinline__ bf16x8 cat8(bf16x4 lo, bf16x4 hi) {

@@ -36,6 +36,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "../../include/msenv.h"
 #include "../../include/mscnn.h"
 #include "mscnn_common.h"
@@ -77,6 +79,9 @@ struct TrunkFwdParams {
   const E* x0;  // [N][P][96] block 0's input
   E* ws;        // [grid][P][96]: block outputs that are not kept (residual of the next block)
   unsigned long long* diag;  // MC_DIAG builds: per-wave phase cycle totals [grid][4][8]
+#ifdef MC_DIAG
+  int dflags;  // timing experiments only: bit 0 drops the epilogue's global stores
+#endif
   float* pooled;  // [N][96] or null: the last layer's output averaged over the pixels
   int NL, N, H, W;
   float eps;
@@ -358,6 +363,13 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_fwd(TrunkFwdPar
       if (!out && (l & 1) && more) out = p.ws + (size_t)blockIdx.x * P * COUT;  // the next block's residual
       E* ysave = p.L[l].ysave ? p.L[l].ysave + so : nullptr;
       uint8_t* rmask = p.L[l].rmask ? p.L[l].rmask + (size_t)n * P * C8 : nullptr;
+#ifdef MC_DIAG
+      if (p.dflags & 1) {
+        out = nullptr;
+        ysave = nullptr;
+        rmask = nullptr;
+      }
+#endif
       float ca[3][8], cb[3][8], cd[3][8];
 #pragma unroll
       for (int j3 = 0; j3 < 3; ++j3) {
@@ -674,6 +686,13 @@ __global__ __launch_bounds__(512, 1) void k_trunk_fwd2(TrunkFwdParams<E> p) {
       E* out = !valid ? nullptr : (p.L[l].out ? p.L[l].out + so : ((l & 1) && more ? wsl : nullptr));
       E* ysave = p.L[l].ysave && valid ? p.L[l].ysave + so : nullptr;
       uint8_t* rmask = p.L[l].rmask && valid ? p.L[l].rmask + (size_t)n * P * C8 : nullptr;
+#ifdef MC_DIAG
+      if (p.dflags & 1) {
+        out = nullptr;
+        ysave = nullptr;
+        rmask = nullptr;
+      }
+#endif
       float ca[3][8], cb[3][8], cd[3][8];
 #pragma unroll
       for (int j3 = 0; j3 < 3; ++j3) {
@@ -734,6 +753,518 @@ __global__ __launch_bounds__(512, 1) void k_trunk_fwd2(TrunkFwdParams<E> p) {
 }
 
 // ------------------------------------------------------------------------------------
+// k_trunk_fwd_pp (boards of <= 256 cells, <= 10 layers): the forward of k_trunk_fwd2 re-scheduled
+// so that the matrix pipe never waits for the GroupNorm / epilogue work. Two 4-wave teams per
+// 512-thread workgroup (one per CU), one sample each, run PING-PONG: while team A runs the 9 taps
+// of a layer on the MFMA, team B runs the statistics and epilogue of its previous layer on the
+// VALU, then they swap. A half-period is 9 intervals, one per tap of the MFMA team, each closed by
+// one workgroup barrier; the epilogue team cuts its work into the same 9 intervals:
+//   P0 GroupNorm pass 1 (sums) | P1 pass 2 (squared deviations) | P2 scale / shift / dropout
+//   coefficients | P3 .. P8 the epilogue, one (channel tile, pixel tile) piece per interval.
+// Differences to k_trunk_fwd2 that make the epilogue cheap enough to hide:
+//  * swapped MFMA operands: D[co][px] = W[co] . X[px], so a lane holds ONE pixel and 4-channel
+//    runs of the output; the epilogue works on the accumulators in place (no y -> LDS pass, no
+//    chunk re-read) and writes 8-byte pieces: the next layer's tile (ds_write_b64), y / out
+//    (global 8-B stores) and the ReLU bits (12 bytes a pixel after one lane exchange);
+//  * the accumulators start from the conv bias (y = b + sum, staged bias table in LDS);
+//  * tiles and weight taps are 192-B rows with the 16-B chunk index XOR-ed by (row >> 2) & 3
+//    (conflict-free ds_read_b128 without padding), so two sample tiles and a 3-slot weight ring
+//    fit: taps arrive by LDS-DMA two intervals ahead (global_load_lds gathers the swizzle), waited
+//    with a counted vmcnt by the issuing wave, never behind the epilogue's stores;
+//  * the next sample's input is gathered into the tile by LDS-DMA during the last layer's
+//    statistics, and the value head's average pool is reduced from registers.
+// The weight stream repeats each layer's taps for the second team (L0 L0 L1 L1 ...: position
+// s = 9 h + tap of half-period h holds layer (h >> 1) % NL, tap s % 9, ring slot s % 3 = tap % 3).
+// Arithmetic per element is k_trunk_fwd2's; the f32 sums run in another order (statistics over
+// the lanes of a pixel-major layout), so results agree with the per-layer kernels to rounding
+// (tests/test_trunk_gpu.py), not bitwise.
+constexpr int PPRS = COUT * 2;           // tile / tap row bytes (12 chunks of 16 B, swizzled)
+constexpr int PP_TAPB = COUT * PPRS;     // one weight tap: 18,432 B = 18 LDS-DMA pieces of 1 KiB
+constexpr int PP_TAPP = PP_TAPB / 1024;
+constexpr int PP_MAXL = 10;
+constexpr int PP_SLOTS = 3;
+constexpr int PP_RED = 2 * 2 * WAVES * 8;  // sRed [team][pass][wave][8] f32
+
+__host__ __device__ inline int pp_tile(int P) { return ((P + 1) * PPRS + 15) & ~15; }
+__host__ __device__ inline size_t pp_lds(int P) {
+  return 2 * (size_t)pp_tile(P) + PP_SLOTS * PP_TAPB + (PP_MAXL * COUT + PP_RED + 2 * 3 * COUT + 2 * WAVES * COUT) * 4;
+}
+// byte offset of 16-B chunk c of row r in a swizzled [rows][192 B] image
+__device__ __forceinline__ int pp_swz(int r, int c) { return r * PPRS + ((c ^ ((r >> 2) & 3)) << 4); }
+
+__device__ __forceinline__ uint32_t pp_lds_addr(const void* p) {
+  return (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)(p);
+}
+// one full-wave LDS-DMA, 16 B a lane, lane-linear at LDS byte address m0v, from a wave-uniform
+// base plus this lane's 32-bit byte offset (inline asm: the compiler puts no waits on LDS reads)
+__device__ __forceinline__ void pp_dma(const void* base, uint32_t off, uint32_t m0v) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(base), "s"(m0v)
+               : "memory", "m0");
+}
+template <int N>
+__device__ __forceinline__ void pp_wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt(0x0F70 | (N & 15) | ((N >> 4) << 14));
+}
+
+// per-lane coordinates, re-derived at the top of every phase from an opaque thread index: nothing
+// computed from them is hoisted out of the half-period loop (it would stay live across both
+// phases and spill)
+struct PPLane {
+  int ttid, lane, l32, hh;
+};
+__device__ __forceinline__ PPLane pp_lane() {
+  const int tid = (int)threadIdx.x + opaque0();
+  return PPLane{tid & 255, tid & 63, tid & 31, (tid >> 5) & 1};
+}
+
+template <typename E, int NPT, bool FULL, bool SAVE>
+__global__ __launch_bounds__(512, 1) void k_trunk_fwd_pp(TrunkFwdParams<E> p) {
+#pragma clang fp contract(off)
+  typedef typename EV<E>::v8 E8;
+  typedef typename EV<E>::v4 E4;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int H = p.H, W = p.W, P = H * W, NL = p.NL;
+  const int tb = pp_tile(P);
+  const int team = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 8);
+  const int wave = __builtin_amdgcn_readfirstlane(((int)threadIdx.x >> 6) & 3);
+  unsigned char* sTile = smem + team * tb;
+  unsigned char* sRing = smem + 2 * tb;
+  float* sBias = reinterpret_cast<float*>(sRing + PP_SLOTS * PP_TAPB);  // [NL][96]
+  float* sRed = sBias + PP_MAXL * COUT;                                  // [2 team][2 pass][4 wave][8]
+  float* sRedT = sRed + team * 2 * WAVES * 8;                            // this team's [2][4][8]
+  float* sAB = sRed + PP_RED + team * 3 * COUT;                          // this team's [3][96]
+  float* sPool = sRed + PP_RED + 2 * 3 * COUT + team * WAVES * COUT;     // this team's [4][96]
+  const uint32_t ring0 = __builtin_amdgcn_readfirstlane(pp_lds_addr(sRing));
+  const uint32_t tile0 = __builtin_amdgcn_readfirstlane(pp_lds_addr(sTile));
+#ifdef MC_DIAG
+  // per wave: 0 MFMA-phase issue + taps, 1 its vmcnt waits + barriers, 2 P0-P2 work, 3 their barrier
+  // waits, 4 epilogue pieces, 5 their barrier waits, 6 active MFMA intervals, 7 active pieces
+  unsigned long long dacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tlast = __builtin_amdgcn_s_memtime();
+#endif
+
+  // samples: pair k of this workgroup = blockIdx.x + k * grid; team A takes 2 pair, team B 2 pair + 1
+  const int npairs = (p.N + 1) >> 1;
+  const int nA = (npairs - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int lastpair = (int)blockIdx.x + (nA - 1) * (int)gridDim.x;
+  const int nB = 2 * lastpair + 1 < p.N ? nA : nA - 1;
+  const int nS = team ? nB : nA;
+  // half-periods: team h & 1 runs its taps, the other its epilogue
+  const int HP = 2 * nA * NL + 1;
+  // weight-DMA pieces of a tap: the 4 tap waves take pieces wave + 4 i (4-5 each)
+  constexpr int DW = WAVES, DI = (PP_TAPP + DW - 1) / DW, DMIN = PP_TAPP / DW;
+  const int dw = wave;
+  auto sample_of = [&](int k) { return 2 * ((int)blockIdx.x + k * (int)gridDim.x) + team; };
+
+  // x0 of sample n into this team's tile, gathered by LDS-DMA (pieces wave, wave + 4, ...)
+  auto issue_x0 = [&](int n, int lane) {
+    const E* src = p.x0 + (size_t)n * P * COUT;
+    const int npc = (P * PPRS + 1023) >> 10;
+    for (int j = wave; j < npc; j += WAVES) {
+      const int q = j * 1024 + lane * 16;
+      if (q < P * PPRS) {
+        const int r = q / PPRS, cs = (q - r * PPRS) >> 4;
+        pp_dma(src, (uint32_t)(r * PPRS + ((cs ^ ((r >> 2) & 3)) << 4)), tile0 + j * 1024);
+      }
+    }
+  };
+  // weight stream position s, this wave's pieces j = wave + 4 i: layer ((s / 9) >> 1) % NL, tap
+  // s % 9, ring slot s % 3; piece j of a slot holds LDS bytes [j KiB, j KiB + 1 KiB): row co, chunk
+  // slot cs hold source chunk cs ^ ((co >> 2) & 3) of the [96][96] tap
+  auto woffs = [&](int lane, uint32_t (&wo)[DI]) {
+#pragma unroll
+    for (int i = 0; i < DI; ++i) {
+      const int j = dw + DW * i, q = j * 1024 + lane * 16, co = q / PPRS, cs = (q - co * PPRS) >> 4;
+      wo[i] = (uint32_t)(co * PPRS + ((cs ^ ((co >> 2) & 3)) << 4));
+    }
+  };
+  auto issue_w = [&](int s, const uint32_t (&wo)[DI]) {
+    const int hs = s / 9, ts = s - hs * 9, ls = (hs >> 1) % NL;
+    const E* base = p.L[ls].wt + (size_t)ts * COUT * COUT;
+    const uint32_t sb = ring0 + (uint32_t)((s % PP_SLOTS) * PP_TAPB);
+#pragma unroll
+    for (int i = 0; i < DI; ++i) {
+      const int j = dw + DW * i;
+      if (j < PP_TAPP) pp_dma(base, wo[i], sb + j * 1024);
+    }
+  };
+
+  // ---------------- prologue ----------------
+  {
+    const PPLane ln = pp_lane();
+    for (int i = threadIdx.x; i < 2 * 12; i += 512) {  // the zero row P of both tiles
+      const int tm = i / 12, c = i - tm * 12;
+      *reinterpret_cast<u32x4*>(smem + tm * tb + P * PPRS + c * 16) = u32x4{0u, 0u, 0u, 0u};
+    }
+    for (int i = threadIdx.x; i < NL * COUT; i += 512) sBias[i] = p.L[i / COUT].bias[i % COUT];
+    if (nS > 0) issue_x0(sample_of(0), ln.lane);
+    uint32_t wo[DI];
+    woffs(ln.lane, wo);
+    issue_w(team, wo);  // stream positions 0 (team A's waves) and 1 (team B's)
+    pp_wait_vm<0>();
+    __syncthreads();
+  }
+
+  f32x16 acc[NPT][3];
+  int pool_n = -1;  // sample whose pooled sums wait in sPool
+  for (int h = 0; h < HP; ++h) {
+    const int m = h & 1, j = h >> 1;
+    if (team == m) {
+      // ======================= MFMA phase: step j of this team =======================
+      __builtin_amdgcn_s_setprio(1);
+      const PPLane ln = pp_lane();
+      uint32_t wo[DI];
+      woffs(ln.lane, wo);
+      const bool act_rt = j < nS * NL;
+      const int l = act_rt ? j % NL : 0;
+      if (pool_n >= 0) {  // the previous sample's pooled mean (sPool complete since the last barrier)
+        if (ln.ttid < COUT) {
+          const int c = ln.ttid;
+          p.pooled[(size_t)pool_n * COUT + c] =
+              ((sPool[c] + sPool[COUT + c]) + (sPool[2 * COUT + c] + sPool[3 * COUT + c])) * (1.0f / (float)P);
+        }
+        pool_n = -1;
+      }
+      // weight A-operand rows co = ct * 32 + l32: chunk 2 ks ^ vw (even ks at wa0 + 32 ks, odd ks at
+      // wa1 + 32 (ks - 1)); this lane's output pixel per 32-pixel tile (past P: the zero row)
+      const int vw = ((ln.l32 >> 2) & 3) ^ ln.hh;
+      const int wa0 = ln.l32 * PPRS + (vw << 4), wa1 = ln.l32 * PPRS + ((vw ^ 2) << 4);
+      int qr[NPT], qc[NPT];
+#pragma unroll
+      for (int t = 0; t < NPT; ++t) {
+        const int q = (wave * NPT + t) * 32 + ln.l32;
+        qr[t] = q < P ? q / W : -1000;
+        qc[t] = q < P ? q - qr[t] * W : -1000;
+      }
+      // (specialised on act: the compiler's vmcnt bookkeeping must not see a path on which the
+      // epilogue's loads are still pending, or it waits for vmcnt(0) -- the weight DMAs -- every tap)
+      auto taps = [&](auto ACT) {
+      constexpr bool act = decltype(ACT)::value;
+      if (act) {  // the accumulators start from the conv bias (channel ct * 32 + 8 (i >> 2) + 4 hh + (i & 3))
+#pragma unroll
+        for (int ct = 0; ct < 3; ++ct)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 b4 = *reinterpret_cast<const f32x4*>(&sBias[l * COUT + ct * 32 + 8 * g + 4 * ln.hh]);
+#pragma unroll
+            for (int t = 0; t < NPT; ++t)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) acc[t][ct][4 * g + e] = b4[e];
+          }
+      }
+#pragma nounroll
+      for (int tap3 = 0; tap3 < 9; tap3 += 3)
+#pragma unroll
+        for (int ts = 0; ts < 3; ++ts) {
+          const int tap = tap3 + ts;
+          const int s = 9 * h + tap;
+          const bool iss = s + 2 < 9 * HP;
+          if (iss) issue_w(s + 2, wo);
+          if (act) {
+            const int dr = tap / 3 - 1, dc = tap % 3 - 1;
+            int xa0[NPT], xa1[NPT];
+#pragma unroll
+            for (int t = 0; t < NPT; ++t) {
+              const int sr = qr[t] + dr, sc = qc[t] + dc;
+              const bool v = (unsigned)sr < (unsigned)H && (unsigned)sc < (unsigned)W;
+              const int r = v ? sr * W + sc : P;
+              const int xv = ((r >> 2) & 3) ^ ln.hh;
+              xa0[t] = r * PPRS + (xv << 4);
+              xa1[t] = r * PPRS + ((xv ^ 2) << 4);
+            }
+            const unsigned char* sw = sRing + ts * PP_TAPB;  // slot s % 3 = tap % 3
+            constexpr int KS = COUT / 16;
+            E8 A[2][3], B[2][NPT];
+            auto ld = [&](int ks, E8 (&a)[3], E8 (&b)[NPT]) {
+              const int wo = (ks & 1) ? wa1 + 32 * (ks - 1) : wa0 + 32 * ks;
+#pragma unroll
+              for (int ct = 0; ct < 3; ++ct) a[ct] = *reinterpret_cast<const E8*>(sw + wo + ct * 32 * PPRS);
+#pragma unroll
+              for (int t = 0; t < NPT; ++t)
+                b[t] = *reinterpret_cast<const E8*>(sTile + ((ks & 1) ? xa1[t] + 32 * (ks - 1) : xa0[t] + 32 * ks));
+            };
+            ld(0, A[0], B[0]);
+            __builtin_amdgcn_sched_group_barrier(0x100, NPT + 3, 0);
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+              if (ks + 1 < KS) {
+                ld(ks + 1, A[(ks + 1) & 1], B[(ks + 1) & 1]);
+                __builtin_amdgcn_sched_group_barrier(0x100, NPT + 3, 0);
+              }
+#pragma unroll
+              for (int ct = 0; ct < 3; ++ct)
+#pragma unroll
+                for (int t = 0; t < NPT; ++t) acc[t][ct] = mfma32(A[ks & 1][ct], B[ks & 1][t], acc[t][ct]);
+              __builtin_amdgcn_sched_group_barrier(0x008, 3 * NPT, 0);
+            }
+          }
+          TSTAMP(0);
+#ifdef MC_DIAG
+          dacc[6] += act ? 1 : 0;
+#endif
+          // position s + 1 must have landed: issued by this wave one interval ago (tap >= 1), or by
+          // the other team at its last tap (it waits for it at the top of its epilogue phase)
+          if (tap >= 1) {
+            if (iss) pp_wait_vm<DMIN>();  // this interval's pieces may stay in flight
+            else pp_wait_vm<0>();
+          }
+          lds_barrier();
+          TSTAMP(1);
+        }
+      };
+      if (act_rt) taps(std::true_type{});
+      else taps(std::false_type{});
+      __builtin_amdgcn_s_setprio(0);
+    } else {
+      // =================== epilogue phase: step jp of this team ===================
+      const int jp = m ? j : j - 1;
+      const bool act_rt = jp >= 0 && jp < nS * NL;
+      auto post = [&](auto ACT) {
+      constexpr bool act = decltype(ACT)::value;
+      const int k = act ? jp / NL : 0, l = act ? jp % NL : 0;
+      const int n = act ? sample_of(k) : 0;
+      const size_t so = (size_t)n * P * COUT;
+      const bool last = l == NL - 1;
+      const float inv_cnt = 1.0f / (16.0f * (float)P);
+      // ---- P0: GroupNorm sums; the residual, the GN parameters, the next sample's input in flight ----
+      pp_wait_vm<0>();  // weight pieces this wave issued at its last tap (the MFMA team's tap 0 needs them)
+      // the residual (block input) of a conv2 layer: piece q's 4 x 8 B, loaded two pieces ahead (P0
+      // loads pieces 0 and 1) into a 3-deep register ring, always before the stores they pass
+      const E* res = nullptr;
+      u32x2 rv[3][4];
+      auto load_res = [&](int q) {
+        const PPLane ln = pp_lane();
+        const int t = q % NPT, ct = q / NPT;
+        const int px = (wave * NPT + t) * 32 + ln.l32;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          rv[q % 3][g] = u32x2{0u, 0u};
+          if (res && (FULL || px < P))
+            rv[q % 3][g] = *reinterpret_cast<const u32x2*>(res + (size_t)px * COUT + ct * 32 + 8 * g + 4 * ln.hh);
+        }
+      };
+      float gmv = 0.f, btv = 0.f, dmv = 1.f;
+      {
+        const PPLane ln = pp_lane();
+        if (act) {
+          if (last && k + 1 < nS) issue_x0(sample_of(k + 1), ln.lane);
+          if (l & 1) res = l == 1 ? p.x0 + so : (p.L[l - 2].out ? p.L[l - 2].out + so : p.ws + ((size_t)blockIdx.x * 2 + team) * P * COUT);
+#ifdef MC_DIAG
+          if (p.dflags & 2) res = nullptr;
+#endif
+          load_res(0);
+          load_res(1);
+          if (ln.ttid < COUT) {
+            gmv = p.L[l].gamma[ln.ttid];
+            btv = p.L[l].beta[ln.ttid];
+            if (p.L[l].dmask) dmv = p.L[l].dmask[(size_t)n * COUT + ln.ttid];
+          }
+          float s6[NGRP];
+#pragma unroll
+          for (int ct = 0; ct < 3; ++ct)
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+              float v = 0.f;
+#pragma unroll
+              for (int t = 0; t < NPT; ++t) {
+                const int px = (wave * NPT + t) * 32 + ln.l32;
+                float u = 0.f;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) u += acc[t][ct][8 * hf + i];
+                v += (FULL || px < P) ? u : 0.f;
+              }
+              s6[2 * ct + hf] = wave_sum(v);
+            }
+          if (ln.lane == 0) {
+#pragma unroll
+            for (int g = 0; g < NGRP; ++g) sRedT[wave * 8 + g] = s6[g];
+          }
+        }
+      }
+      TSTAMP(2);
+      lds_barrier();
+      TSTAMP(3);
+      // ---- P1: means, GroupNorm squared deviations ----
+      if (act) {
+        const PPLane ln = pp_lane();
+        float s6[NGRP];
+#pragma unroll
+        for (int ct = 0; ct < 3; ++ct)
+#pragma unroll
+          for (int hf = 0; hf < 2; ++hf) {
+            const int g = 2 * ct + hf;
+            const float mu = ((sRedT[g] + sRedT[8 + g]) + (sRedT[16 + g] + sRedT[24 + g])) * inv_cnt;
+            float v = 0.f;
+#pragma unroll
+            for (int t = 0; t < NPT; ++t) {
+              const int px = (wave * NPT + t) * 32 + ln.l32;
+              float u = 0.f;
+#pragma unroll
+              for (int i = 0; i < 8; ++i) {
+                const float d = acc[t][ct][8 * hf + i] - mu;
+                u = __builtin_fmaf(d, d, u);
+              }
+              v += (FULL || px < P) ? u : 0.f;
+            }
+            s6[g] = wave_sum(v);
+          }
+        if (ln.lane == 0) {
+#pragma unroll
+          for (int g = 0; g < NGRP; ++g) sRedT[32 + wave * 8 + g] = s6[g];
+        }
+      }
+      TSTAMP(2);
+      lds_barrier();
+      TSTAMP(3);
+      // ---- P2: scale / shift / dropout coefficients per channel (threads c < 96: group c >> 4) ----
+      pp_wait_vm<0>();  // residual, GN parameters, the next sample's input
+      if (act) {
+        const PPLane ln = pp_lane();
+        if (ln.ttid < COUT) {
+          const int g = ln.ttid >> 4;
+          const float mu = ((sRedT[g] + sRedT[8 + g]) + (sRedT[16 + g] + sRedT[24 + g])) * inv_cnt;
+          const float rs = rsqrtf(((sRedT[32 + g] + sRedT[40 + g]) + (sRedT[48 + g] + sRedT[56 + g])) * inv_cnt + p.eps);
+          const float a = gmv * rs;
+          sAB[ln.ttid] = a;
+          sAB[COUT + ln.ttid] = btv - mu * a;
+          sAB[2 * COUT + ln.ttid] = dmv;
+          float* stats = p.L[l].stats;
+          if (SAVE && (ln.ttid & 15) == 0) {
+            stats[((size_t)n * NGRP + g) * 2 + 0] = mu;
+            stats[((size_t)n * NGRP + g) * 2 + 1] = rs;
+          }
+        }
+      }
+      TSTAMP(2);
+      lds_barrier();
+      TSTAMP(3);
+      // ---- P3 .. P8: the epilogue, piece q = (ct, t) per interval (NPT = 1: P6 .. P8 idle) ----
+      E* out = nullptr;
+      E* ysave = nullptr;
+      uint8_t* rmask = nullptr;
+      bool pool_here = false;
+      if (act) {
+        out = p.L[l].out ? p.L[l].out + so
+                         : ((l & 1) && !last ? p.ws + ((size_t)blockIdx.x * 2 + team) * P * COUT : nullptr);
+        ysave = SAVE ? p.L[l].ysave + so : nullptr;  // SAVE: every layer has ysave, stats, relu_mask
+        rmask = SAVE ? p.L[l].rmask + (size_t)n * P * C8 : nullptr;
+        pool_here = last && p.pooled;
+#ifdef MC_DIAG
+        if (p.dflags & 1) {
+          if (!last) out = nullptr;
+        }
+#endif
+      }
+      uint32_t rw[NPT][3];
+      // the pieces, specialised on the value head's pool (the last layer only)
+      auto pieces = [&](auto POOL) {
+      constexpr bool pool = decltype(POOL)::value;
+      float pl[16];
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        if (q < 3 * NPT && act) {
+          const int ct = q / NPT, t = q % NPT;
+          if (q + 2 < 3 * NPT) load_res(q + 2);
+          const PPLane ln = pp_lane();
+          const int px = (wave * NPT + t) * 32 + ln.l32;
+          const bool pv = FULL || px < P;
+          uint32_t word = 0u;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int co = ct * 32 + 8 * g + 4 * ln.hh;
+            const f32x4 ca = *reinterpret_cast<const f32x4*>(&sAB[co]);
+            const f32x4 cb = *reinterpret_cast<const f32x4*>(&sAB[COUT + co]);
+            const f32x4 cd = *reinterpret_cast<const f32x4*>(&sAB[2 * COUT + co]);
+            const E4 rh = __builtin_bit_cast(E4, rv[q % 3][g]);
+            E4 yh, oh;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              yh[e] = (E)acc[t][ct][4 * g + e];
+              const float z = fmaxf(__builtin_fmaf((float)yh[e], ca[e], cb[e]) + (float)rh[e], 0.f);
+              oh[e] = (E)pin_f32(z * cd[e]);
+            }
+            uint32_t nib = 0u;  // ReLU bits of the 16-bit outputs
+#pragma unroll
+            for (int e = 0; e < 4; ++e) nib |= ((float)oh[e] > 0.f ? 1u : 0u) << e;
+            word |= nib << (8 * g + 4 * ln.hh);
+            const size_t go = (size_t)px * COUT + co;
+            if (pv) {
+              if (SAVE) *reinterpret_cast<u32x2*>(ysave + go) = __builtin_bit_cast(u32x2, yh);
+              if (!last) *reinterpret_cast<u32x2*>(sTile + pp_swz(px, ct * 4 + g) + ln.hh * 8) = __builtin_bit_cast(u32x2, oh);
+              if (out) *reinterpret_cast<u32x2*>(out + go) = __builtin_bit_cast(u32x2, oh);
+            }
+            if (pool) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float o = pv ? (float)oh[e] : 0.f;
+                pl[4 * g + e] = t == 0 ? o : pl[4 * g + e] + o;
+              }
+            }
+          }
+          rw[t][ct] = word;
+          if (pool && t == NPT - 1) {  // this channel tile's sums over the wave's pixels -> sPool (lanes 31, 63)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              float v = row_sum16(pl[i]);
+              v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x142, 0xA, 0xf, false));
+              pl[i] = v;
+            }
+            if (ln.l32 == 31) {
+#pragma unroll
+              for (int g = 0; g < 4; ++g)
+                *reinterpret_cast<f32x4*>(&sPool[wave * COUT + ct * 32 + 8 * g + 4 * ln.hh]) =
+                    f32x4{pl[4 * g], pl[4 * g + 1], pl[4 * g + 2], pl[4 * g + 3]};
+            }
+          }
+        }
+        if (q == 5 && act && SAVE) {  // ReLU bits: byte ct * 4 + g = low nibble (hh 0) | high nibble (hh 1)
+          const PPLane ln = pp_lane();
+#pragma unroll
+          for (int t = 0; t < NPT; ++t) {
+            const int px = (wave * NPT + t) * 32 + ln.l32;
+            uint32_t b3[3];
+#pragma unroll
+            for (int ct = 0; ct < 3; ++ct) b3[ct] = rw[t][ct] | (uint32_t)__shfl_xor((int)rw[t][ct], 32);
+            if (ln.hh == 0 && (FULL || px < P)) {
+              uint32_t* rp = reinterpret_cast<uint32_t*>(rmask + (size_t)px * C8);
+              rp[0] = b3[0];
+              rp[1] = b3[1];
+              rp[2] = b3[2];
+            }
+          }
+        }
+        if (q == 5 && pool && act) pool_n = n;
+        TSTAMP(4);
+#ifdef MC_DIAG
+        dacc[7] += (q < 3 * NPT && act) ? 1 : 0;
+#endif
+        lds_barrier();
+        TSTAMP(5);
+      }
+      };
+      if (pool_here) pieces(std::true_type{});
+      else pieces(std::false_type{});
+      };
+      if (act_rt) post(std::true_type{});
+      else post(std::false_type{});
+    }
+  }
+  if (pool_n >= 0) {  // the last sample's pooled mean (sPool complete: the last barrier)
+    const PPLane ln = pp_lane();
+    if (ln.ttid < COUT) {
+      const int c = ln.ttid;
+      p.pooled[(size_t)pool_n * COUT + c] =
+          ((sPool[c] + sPool[COUT + c]) + (sPool[2 * COUT + c] + sPool[3 * COUT + c])) * (1.0f / (float)P);
+    }
+  }
+#ifdef MC_DIAG
+  if (p.diag && (threadIdx.x & 63) == 0)
+    for (int q = 0; q < 8; ++q) p.diag[((size_t)blockIdx.x * 8 + (threadIdx.x >> 6)) * 8 + q] = dacc[q];
+#endif
+}
+
+// ------------------------------------------------------------------------------------
 template <typename E>
 struct TBLayer {
   const E* y;              // ysave of the forward
@@ -751,6 +1282,9 @@ struct TrunkBwdParams {
   E* ws;          // [grid][P][96]: a block's skip gradient between its conv2 and its input
   float* part;    // [VG][NL][3][96] d gamma, d beta, d bias per partial row
   unsigned long long* diag;  // MC_DIAG builds: per-wave phase cycle totals [grid][4][8]
+#ifdef MC_DIAG
+  int dflags;  // timing experiments only: bit 0 drops pass 2's global stores (dy, skip slot)
+#endif
   int NL, N, H, W;
   int VG;         // partial rows: the per-layer kernel's grid (min(N, 2 x CUs)), so the sums match it
   TBLayer<E> L[MAXL + 1];
@@ -980,7 +1514,11 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_bwd(TrunkBwdPar
           if (px < P) {
             E* sp = &sD[px * DCP + c8 * 8];
             const u32x4 zv = *reinterpret_cast<const u32x4*>(sp);
+#ifdef MC_DIAG
+            if (keep_dz && !(p.dflags & 1)) *reinterpret_cast<u32x4*>(&wsl[(size_t)px * COUT + c8 * 8]) = zv;
+#else
             if (keep_dz) *reinterpret_cast<u32x4*>(&wsl[(size_t)px * COUT + c8 * 8]) = zv;
+#endif
             const E8 z8 = __builtin_bit_cast(E8, zv);
             const E8 y8 = __builtin_bit_cast(E8, yr[i]);
             E8 d8;
@@ -988,6 +1526,9 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_bwd(TrunkBwdPar
             for (int j = 0; j < 8; ++j) d8[j] = (E)__builtin_fmaf(A[j], (float)z8[j], __builtin_fmaf(Bg, (float)y8[j], Cg));
             const u32x4 v = __builtin_bit_cast(u32x4, d8);
             *reinterpret_cast<u32x4*>(sp) = v;
+#ifdef MC_DIAG
+            if (!(p.dflags & 1))
+#endif
             *reinterpret_cast<u32x4*>(&dyp[(size_t)px * COUT + c8 * 8]) = v;
           }
         }
@@ -1031,11 +1572,13 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_bwd(TrunkBwdPar
 #pragma unroll
           for (int t = 0; t < NPT; ++t) a[t] = *reinterpret_cast<const E8*>(&sD[aoff[t] + k0]);
         };
+        // swapped operands: D[ci][px] = W^T[ci] . dy[px], so a lane holds one pixel and 4-channel runs
+        // of dx (each element the same products in the same order as D[px][ci])
         auto mm = [&](const E8 (&a)[NPT], const E8 (&b)[3]) {
 #pragma unroll
           for (int t = 0; t < NPT; ++t)
 #pragma unroll
-            for (int ct = 0; ct < 3; ++ct) acc[t][ct] = mfma32(a[t], b[ct], acc[t][ct]);
+            for (int ct = 0; ct < 3; ++ct) acc[t][ct] = mfma32(b[ct], a[t], acc[t][ct]);
         };
         E8 a0[NPT], b0[3], a1[NPT], b1[3];
         ld(0, a0, b0);
@@ -1067,16 +1610,23 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_bwd(TrunkBwdPar
         }
       }
       TSTAMP(3);
-      // dx -> the tile (16-bit, as the per-layer kernel's dx store): layer li-1's dout
+      // dx -> the tile (16-bit, as the per-layer kernel's dx store): layer li-1's dout; lane = pixel,
+      // channels ct * 32 + 8 g + 4 hh + 0..3 as one 8-byte write
 #pragma unroll
-      for (int t = 0; t < NPT; ++t)
+      for (int t = 0; t < NPT; ++t) {
+        const int px = (wave * NPT + t) * 32 + l32;
+        if (px < P) {
 #pragma unroll
-        for (int ct = 0; ct < 3; ++ct)
+          for (int ct = 0; ct < 3; ++ct)
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int px = (wave * NPT + t) * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-            if (px < P) sD[px * DCP + ct * 32 + l32] = (E)acc[t][ct][i];
-          }
+            for (int g = 0; g < 4; ++g) {
+              typename EV<E>::v4 d4;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) d4[e] = (E)acc[t][ct][4 * g + e];
+              *reinterpret_cast<u32x2*>(&sD[px * DCP + ct * 32 + 8 * g + 4 * hh]) = __builtin_bit_cast(u32x2, d4);
+            }
+        }
+      }
       __syncthreads();
       TSTAMP(4);
     }
@@ -1121,6 +1671,15 @@ int trunk_grid(int n, size_t lds) {
 }
 // k_trunk_fwd2 (P <= 256): one 512-thread workgroup per CU, two samples each
 inline bool fwd_two(int P) { return P <= 256; }
+// which forward for P <= 256 cells: MCV_TRUNK_FWD variant 0 (default) = k_trunk_fwd_pp for the no-grad
+// forward (the rollout's; 5-6 % faster, same-box A/B, profiles/r06/trunk_fwd_pp_ab.txt) and
+// k_trunk_fwd2 for the saving forward (bitwise the per-layer kernels, and 5 % faster there);
+// variant 1 = k_trunk_fwd2 always, variant 2 = k_trunk_fwd_pp always
+inline bool fwd_pp(int P, int nl, bool save) {
+  if (P > 256 || nl > PP_MAXL) return false;
+  const int v = g_variant[MCV_TRUNK_FWD];
+  return v == 2 || (v == 0 && !save);
+}
 int trunk_grid2(int n) {
   const int pairs = (n + 1) / 2, cap = num_cus();
   return pairs < cap ? pairs : cap;
@@ -1152,6 +1711,7 @@ int launched(const char* what) {
 
 #ifdef MC_DIAG
 unsigned long long* g_trunk_diag[2] = {nullptr, nullptr};
+int g_trunk_dflags = 0;
 #endif
 
 template <typename E, int NPT, bool FULL>
@@ -1161,6 +1721,19 @@ int launch_trunk_fwd(const TrunkFwdParams<E>& p, hipStream_t s) {
   const size_t lds = tf_lds(p.H * p.W);
   hipLaunchKernelGGL((k_trunk_fwd<E, NPT, FULL>), dim3(trunk_grid(p.N, lds)), dim3(256), lds, s, p);
   return launched("k_trunk_fwd");
+}
+
+template <typename E, int NPT, bool FULL, bool SAVE>
+int launch_trunk_fwd_pp_k(const TrunkFwdParams<E>& p, hipStream_t s) {
+  static bool attr = false;
+  lds_attr_once(k_trunk_fwd_pp<E, NPT, FULL, SAVE>, attr);
+  hipLaunchKernelGGL((k_trunk_fwd_pp<E, NPT, FULL, SAVE>), dim3(trunk_grid2(p.N)), dim3(512), pp_lds(p.H * p.W), s, p);
+  return launched("k_trunk_fwd_pp");
+}
+// SAVE: every layer has ysave, stats and relu_mask (the training forward); otherwise none has
+template <typename E, int NPT, bool FULL>
+int launch_trunk_fwd_pp(const TrunkFwdParams<E>& p, hipStream_t s) {
+  return p.L[0].ysave ? launch_trunk_fwd_pp_k<E, NPT, FULL, true>(p, s) : launch_trunk_fwd_pp_k<E, NPT, FULL, false>(p, s);
 }
 
 template <typename E, int NPT, bool FULL>
@@ -1186,6 +1759,7 @@ int run_trunk_fwd(const uint16_t* x0, const mc_fwd_layer* layers, int nl, void* 
   p.eps = eps;
 #ifdef MC_DIAG
   p.diag = g_trunk_diag[0];
+  p.dflags = g_trunk_dflags;
 #endif
   for (int l = 0; l < nl; ++l) {
     const mc_fwd_layer& a = layers[l];
@@ -1204,6 +1778,16 @@ int run_trunk_fwd(const uint16_t* x0, const mc_fwd_layer* layers, int nl, void* 
   // no-grad forward at 16x16 and 2-6 % at 9x9; on the saving forward at 16x16 it was level while
   // every conv1 output was stored, and is 0.4 ms a minibatch faster since they are recomputed in
   // the weight gradient instead (profiles/r05/trunk_fwd2_save_ab.txt)
+  bool uniform = true;  // k_trunk_fwd_pp: saves on every layer or on none
+  for (int l = 0; l < nl; ++l)
+    uniform &= (layers[l].ysave != nullptr) == (layers[0].ysave != nullptr) &&
+               (layers[l].stats != nullptr) == (layers[0].ysave != nullptr) &&
+               (layers[l].relu_mask != nullptr) == (layers[0].ysave != nullptr);
+  if (fwd_pp(P, nl, layers[0].ysave != nullptr) && uniform) {
+    if (P == 256) return launch_trunk_fwd_pp<E, 2, true>(p, s);
+    if (P == 128) return launch_trunk_fwd_pp<E, 1, true>(p, s);
+    return P < 128 ? launch_trunk_fwd_pp<E, 1, false>(p, s) : launch_trunk_fwd_pp<E, 2, false>(p, s);
+  }
   if (fwd_two(P)) {
     if (P == 256) return launch_trunk_fwd2<E, 2, true>(p, s);
     return P <= 128 ? launch_trunk_fwd2<E, 1, false>(p, s) : launch_trunk_fwd2<E, 2, false>(p, s);
@@ -1239,6 +1823,7 @@ int run_trunk_bwd(const uint16_t* dout, const mc_bwd_layer* layers, int nl, floa
   p.VG = trunk_vgrid(n);
 #ifdef MC_DIAG
   p.diag = g_trunk_diag[1];
+  p.dflags = g_trunk_dflags;
 #endif
   p.NL = nl;
   p.N = n;
@@ -1287,6 +1872,7 @@ void mc_set_trunk_diag(unsigned long long* fwd, unsigned long long* bwd) {
   g_trunk_diag[0] = fwd;
   g_trunk_diag[1] = bwd;
 }
+void mc_set_trunk_dflags(int f) { g_trunk_dflags = f; }
 #endif
 
 int64_t mc_trunk_fwd_workspace(int32_t n, int32_t h, int32_t w_) {

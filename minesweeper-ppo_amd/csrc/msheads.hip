@@ -274,8 +274,8 @@ __device__ __forceinline__ void heads_issue(const HeadBwdParams<E>& p, HeadSlot<
       int64_t q = (base / p.P) * C + (WV - 2) * 256 + lane * 4;
       q = q + 4 <= nfl ? q : nfl - 4;
       dma_x4(p.gadd + q, gb);
-    } else {
-      dma_x4_s(p.f, lane * 16, gb);
+    } else {  // a placeholder DMA keeps the per-wave count at four: 1 KiB of W1 (>= 18 KiB), always in bounds
+      dma_x4_s(p.w1, lane * 16, gb);
     }
   }
 }
@@ -674,8 +674,9 @@ int run_heads_bwd(const uint16_t* f, const float* dlp, const float* dlm, const u
   p.diag = g_heads_diag;
 #endif
   // gadd rows by LDS-DMA need a tile to span at most 5 samples (P >= 16); smaller boards read
-  // them with plain loads (correct, slower: the compiler's waits for them also wait for the ring)
-  const int rc = (gadd && P < 16) ? launch_heads_bwd<E, false>(p, grid, s) : launch_heads_bwd<E, true>(p, grid, s);
+  // them with plain loads (correct, slower: the compiler's waits for them also wait for the ring);
+  // without gadd the kernel without gadd DMAs (P is not used then)
+  const int rc = (gadd && P >= 16) ? launch_heads_bwd<E, true>(p, grid, s) : launch_heads_bwd<E, false>(p, grid, s);
   if (rc) return rc;
   hipLaunchKernelGGL(k_heads_reduce, dim3((PART + HR_IB - 1) / HR_IB), dim3(256), 0, s, (const float*)work, grid, dw1,
                      dw2, db1);

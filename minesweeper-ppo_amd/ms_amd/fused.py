@@ -48,6 +48,8 @@ def _check(rc):
 
 
 VARIANT_FWD, VARIANT_BWD, VARIANT_WGRAD = 0, 1, 2  # mc_set_variant kernels (include/msenv_debug.h)
+VARIANT_TRUNK_FWD = 3  # one-launch trunk forward (<= 256 cells): 0 = default (k_trunk_fwd_pp without saves,
+#   k_trunk_fwd2 with), 1 = k_trunk_fwd2 always, 2 = k_trunk_fwd_pp always
 
 
 class kernel_variant:

@@ -109,12 +109,12 @@ def test_set_variant_validates_each_kernel_range():
     lib = L.load()
     sv = lib.mc_set_variant
     sv.argtypes = [ctypes.c_int32, ctypes.c_int32]
-    for kernel, vmax in ((0, 1), (1, 1), (2, 3)):
+    for kernel, vmax in ((0, 1), (1, 1), (2, 3), (3, 2)):
         for v in range(vmax + 1):
             assert sv(kernel, v) == 0
         assert sv(kernel, vmax + 1) != 0 and sv(kernel, -1) != 0
         assert sv(kernel, 0) == 0
-    assert sv(3, 0) != 0
+    assert sv(4, 0) != 0
 
 
 def test_single_hip_runtime_mapped():

@@ -252,6 +252,39 @@ def test_heads_bwd_deterministic(gpu, n, P):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("n,P", [(300, 256), (5, 1), (70, 81)])
+def test_heads_bwd_c_api_null_gadd(gpu, n, P):
+    """mc_heads_bwd called through the C ABI with gadd = NULL and dlm = NULL (both documented as
+    optional, include/mscnn.h) equals the call with gadd = zeros and the mine rows' dl = zeros
+    (gadd = NULL had selected the gadd-DMA kernel). M = 5 rows also covers the
+    placeholder DMA reading in bounds."""
+    from ms_amd import _lib as L
+    from ms_amd import fused as F
+    torch.manual_seed(9)
+    F._heads_bind()
+    M = n * P
+    f = (torch.randn(M, 96, device=gpu) * 0.7).to(torch.float16)
+    w1 = (torch.randn(192, 96, device=gpu) * 0.1).to(torch.float16)
+    b1, w2 = torch.randn(192, device=gpu) * 0.1, torch.randn(192, device=gpu) * 0.1
+    dlp = torch.randn(M, device=gpu)
+
+    def call(gadd, dlm):
+        out = [torch.empty_like(f), torch.empty(192, 96, device=gpu), torch.empty(192, device=gpu),
+               torch.empty(192, device=gpu)]
+        nws = int(F._hbws(M))
+        work = torch.empty(nws, device=gpu)
+        F._check(F._hb(L.ptr(f), L.ptr(dlp), L.ptr(dlm), L.ptr(w1), None, L.ptr(b1), L.ptr(w2), L.ptr(gadd), P,
+                       L.ptr(out[0]), L.ptr(out[1]), L.ptr(out[2]), L.ptr(out[3]), L.ptr(work), nws, M,
+                       F._dt(f), L.stream_ptr(gpu)))
+        torch.cuda.synchronize()
+        return out
+
+    a = call(None, None)
+    b = call(torch.zeros(n, 96, device=gpu), torch.zeros(M, device=gpu))
+    for x, y, nm in zip(a, b, ("df", "dW1", "db1", "dw2")):
+        assert torch.equal(x, y), nm
+
+
 @pytest.mark.parametrize("n,dt", [(32768, torch.float16), (4100, torch.bfloat16), (64, torch.float16)])
 def test_value_mlp_matches_autocast(gpu, n, dt):
     """fused.value_mlp (the value head's MLP with f32 split-K weight gradients): the forward is

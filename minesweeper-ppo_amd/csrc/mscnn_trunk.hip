@@ -889,6 +889,14 @@ __global__ __launch_bounds__(512, 1) void k_trunk_fwd_pp(TrunkFwdParams<E> p) {
       if (j < PP_TAPP) pp_dma(base, wo[i], sb + j * 1024);
     }
   };
+  // the same for a tap whose base pointer and ring slot are known (the MFMA phase's: no divisions)
+  auto issue_wb = [&](const E* base, uint32_t sb, const uint32_t (&wo)[DI]) {
+#pragma unroll
+    for (int i = 0; i < DI; ++i) {
+      const int j = dw + DW * i;
+      if (j < PP_TAPP) pp_dma(base, wo[i], sb + j * 1024);
+    }
+  };
 
   // ---------------- prologue ----------------
   {
@@ -912,12 +920,20 @@ __global__ __launch_bounds__(512, 1) void k_trunk_fwd_pp(TrunkFwdParams<E> p) {
     const int m = h & 1, j = h >> 1;
     if (team == m) {
       // ======================= MFMA phase: step j of this team =======================
+#ifdef MC_DIAG
+      if (p.dflags & 8) __builtin_amdgcn_s_setprio(0);  // experiment: the epilogue team prioritised
+      else if (!(p.dflags & 4)) __builtin_amdgcn_s_setprio(1);  // 4: no priorities
+#else
       __builtin_amdgcn_s_setprio(1);
+#endif
       const PPLane ln = pp_lane();
       uint32_t wo[DI];
       woffs(ln.lane, wo);
       const bool act_rt = j < nS * NL;
       const int l = act_rt ? j % NL : 0;
+      // the weight stream's layers this half-period (h >> 1) and next ((h + 1) >> 1), mod NL
+      const E* wcur = p.L[(h >> 1) % NL].wt;
+      const E* wnext = p.L[((h + 1) >> 1) % NL].wt;
       if (pool_n >= 0) {  // the previous sample's pooled mean (sPool complete since the last barrier)
         if (ln.ttid < COUT) {
           const int c = ln.ttid;
@@ -960,7 +976,10 @@ __global__ __launch_bounds__(512, 1) void k_trunk_fwd_pp(TrunkFwdParams<E> p) {
           const int tap = tap3 + ts;
           const int s = 9 * h + tap;
           const bool iss = s + 2 < 9 * HP;
-          if (iss) issue_w(s + 2, wo);
+          // position s + 2: tap + 2 of this phase's layer, or tap - 7 of the next phase's; slot (tap + 2) % 3
+          if (iss)
+            issue_wb(tap + 2 < 9 ? wcur + (size_t)(tap + 2) * COUT * COUT : wnext + (size_t)(tap - 7) * COUT * COUT,
+                     ring0 + (uint32_t)(((ts + 2) % PP_SLOTS) * PP_TAPB), wo);
           if (act) {
             const int dr = tap / 3 - 1, dc = tap % 3 - 1;
             int xa0[NPT], xa1[NPT];
@@ -1015,7 +1034,12 @@ __global__ __launch_bounds__(512, 1) void k_trunk_fwd_pp(TrunkFwdParams<E> p) {
       };
       if (act_rt) taps(std::true_type{});
       else taps(std::false_type{});
+#ifdef MC_DIAG
+      if (p.dflags & 8) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+#else
       __builtin_amdgcn_s_setprio(0);
+#endif
     } else {
       // =================== epilogue phase: step jp of this team ===================
       const int jp = m ? j : j - 1;

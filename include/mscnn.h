@@ -88,7 +88,8 @@ int mc_conv_wgrad(const uint16_t* dy, const uint16_t* x, float* dw, float* work,
  * with a = gamma * rstd, b = beta - mean * a per (sample, channel) from its stats [N][6][2] and
  * affine parameters, d = dmask [N][96] (NULL: 1), rounded as the forward epilogue rounds, so dw
  * is bitwise mc_conv_wgrad's on the saved x. The trunk forward then need not write x at all.
- * 16x16 boards (k_wgrad_c96) only; MS_EINVAL otherwise. */
+ * 16x16 boards (k_wgrad_c96, whatever mc_set_variant chose for mc_conv_wgrad) only; MS_EINVAL
+ * otherwise. */
 int mc_conv_wgrad_gn(const uint16_t* dy, const uint16_t* y, const float* stats, const float* gamma, const float* beta,
                      const float* dmask, float* dw, float* work, int64_t work_floats, int32_t n, int32_t h, int32_t w_,
                      int32_t dtype, void* stream);
@@ -130,8 +131,8 @@ int mc_trunk_fwd(const uint16_t* x0, const mc_fwd_layer* layers, int32_t nlayers
                  int32_t n, int32_t h, int32_t w_, float eps, int32_t dtype, void* stream);
 /* mc_trunk_fwd that also writes pooled (f32 [N][96], NULL: not computed) = the last layer's
  * output averaged over the P pixels (the value head's AdaptiveAvgPool2d(1), cnn_residual.py:
- * 97-98), summed in f32 from the output tile while it is still on chip: no second pass over the
- * features. */
+ * 65), summed in f32 on chip (k_trunk_fwd / k_trunk_fwd2: from the last output tile in LDS;
+ * k_trunk_fwd_pp: from the last layer's accumulators): no second pass over the features. */
 int mc_trunk_fwd_pooled(const uint16_t* x0, const mc_fwd_layer* layers, int32_t nlayers, void* work,
                         int64_t work_bytes, float* pooled, int32_t n, int32_t h, int32_t w_, float eps, int32_t dtype,
                         void* stream);

@@ -369,7 +369,6 @@ struct WgradParams {
   const E* x;
   float* part;  // [G][9][96][CIN]
   int N, H, W, G;
-  int exp;  // MC_WSX builds: timing experiments (WGX_* bits; results wrong)
   // x recomputed from a GroupNorm layer's saved y (k_wgrad_c96 only; gn_stats == null: x is x):
   // x = 16-bit(max(y * a + b, 0) * d), a = gamma * rstd, b = beta - mean * a, d = dmask or 1,
   // every step rounded as the forward epilogue that produced x rounds it (mc_conv_wgrad_gn)
@@ -378,16 +377,6 @@ struct WgradParams {
   const float* gn_beta;
   const float* gn_dmask;  // [N][96] or null
 };
-// timing experiments of k_wgrad (libmsenv_wsx.so, mc_set_wgrad_exp; tools/wgrad_exp.py): each bit
-// removes one part so its cost can be read off the launch time
-#ifdef MC_WSX
-#define WGX(bit) ((p.exp & (bit)) != 0)
-int g_wgrad_exp = 0;
-#else
-#define WGX(bit) false
-#endif
-[[maybe_unused]] constexpr int WGX_NO_STAGE = 1, WGX_NO_LOOP = 2, WGX_NO_BAR = 4, WGX_SAME_SAMPLE = 8, WGX_NO_DMA = 16,
-                               WGX_NO_XLOAD = 32;
 
 __host__ __device__ inline int wgrad_lds(int H, int W) {
   const int P = H * W, Ppad = (P + 15) & ~15;
@@ -438,8 +427,7 @@ __device__ __forceinline__ void wgrad_body(const WgradParams<E>& p, E* sDY, E* s
   constexpr int NDY = PF ? 256 * NC8 / 256 : 1, NXS = PF ? 256 * XCH / 256 : 1;
   u32x4 rdy[NDY], rx[NXS];
   auto prefetch = [&](int n) {  // PF: P == 256, W == 16
-    if (n < p.N && !WGX(WGX_NO_STAGE)) {
-      if (WGX(WGX_SAME_SAMPLE)) n = gid;
+    if (n < p.N) {
       const u32x4* dys = reinterpret_cast<const u32x4*>(p.dy + (size_t)n * 256 * COUT);
 #pragma unroll
       for (int k = 0; k < NDY; ++k) rdy[k] = dys[tid + 256 * k];
@@ -453,7 +441,6 @@ __device__ __forceinline__ void wgrad_body(const WgradParams<E>& p, E* sDY, E* s
   if (PF) prefetch(gid);
   for (int n = gid; n < p.N; n += p.G) {
     if (PF) {
-      if (!WGX(WGX_NO_STAGE)) {
 #pragma unroll
       for (int k = 0; k < NDY; ++k) *reinterpret_cast<u32x4*>(&sDY[(tid + 256 * k) * 8]) = rdy[k];
 #pragma unroll
@@ -462,8 +449,7 @@ __device__ __forceinline__ void wgrad_body(const WgradParams<E>& p, E* sDY, E* s
         const int r = px >> 4, cc = px & 15;
         *reinterpret_cast<u32x4*>(&sX[((r + 1) * 18 + cc + 1) * 32 + kk * 8]) = rx[k];
       }
-      }
-      if (!WGX(WGX_NO_BAR)) __syncthreads();
+      __syncthreads();
       prefetch(n + p.G);
       asm volatile("" ::: "memory");  // the prefetch is issued before the MFMA loop
     } else {
@@ -479,8 +465,7 @@ __device__ __forceinline__ void wgrad_body(const WgradParams<E>& p, E* sDY, E* s
       }
       __syncthreads();
     }
-    if (PF && WGX(WGX_NO_LOOP)) {
-    } else if (PF) {
+    if (PF) {
       // 16 pixel steps, operands double-buffered: step k+1's LDS reads are issued
       // before step k's MFMAs
       auto ld = [&](int k0, E8 (&a)[3], E8 (&b)[NTAP]) {
@@ -545,7 +530,7 @@ __device__ __forceinline__ void wgrad_body(const WgradParams<E>& p, E* sDY, E* s
         acc[t] = mfma32(a[tt % 3], b[tt / 3 - TAP0], acc[t]);
       }
     }
-    if (!WGX(WGX_NO_BAR)) __syncthreads();
+    __syncthreads();
   }
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
@@ -643,19 +628,15 @@ __device__ __forceinline__ void wgc_body(const WgradParams<E>& p, E* sDY, E* sX,
   // sample n's dy -> sDY[buf] by LDS-DMA (this wave's 6 KiB: six full-wave 1-KiB instructions,
   // lane-linear destinations) and its x -> registers (6 16-B chunks a thread)
   auto issue = [&](int n, int buf) {
-    if (n < p.N && !WGX(WGX_NO_STAGE)) {
+    if (n < p.N) {
       const E* src = p.dy + (size_t)n * WC_DY;
       const int ln = lane + opaque0();
       const uint32_t dst = (uint32_t)(size_t)((__attribute__((address_space(3))) E*)(sDY + buf * WC_DY)) + WV * 6 * 1024;
-      if (!WGX(WGX_NO_DMA)) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) dma16_asm(src + ((WV * 6 + k) * 64 + ln) * 8, dst + k * 1024);
-      }
-      if (!WGX(WGX_NO_XLOAD)) {
-        const u32x4* xs = reinterpret_cast<const u32x4*>(p.x + (size_t)(WGX(WGX_SAME_SAMPLE) ? gid : n) * WC_DY);
+      for (int k = 0; k < 6; ++k) dma16_asm(src + ((WV * 6 + k) * 64 + ln) * 8, dst + k * 1024);
+      const u32x4* xs = reinterpret_cast<const u32x4*>(p.x + (size_t)n * WC_DY);
 #pragma unroll
-        for (int k = 0; k < 6; ++k) rx[k] = xs[tid + 512 * k];
-      }
+      for (int k = 0; k < 6; ++k) rx[k] = xs[tid + 512 * k];
       if (cact) {
         cm = p.gn_stats[((size_t)n * NGRP + (cc >> 4)) * 2];
         cr = p.gn_stats[((size_t)n * NGRP + (cc >> 4)) * 2 + 1];
@@ -742,8 +723,7 @@ __device__ __forceinline__ void wgc_body(const WgradParams<E>& p, E* sDY, E* sX,
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t] = mfma32(a[T::co(t)], b[T::b(t)], acc[t]);
     };
-    if (WGX(WGX_NO_LOOP)) {
-    } else if constexpr (NT == 10) {
+    if constexpr (NT == 10) {
       // operands double-buffered: step k+1's 14 reads spread between step k's MFMAs
       E8 a0[3], b0[4], a1[3], b1[4];
       ld(0, a0, b0);
@@ -779,7 +759,7 @@ __device__ __forceinline__ void wgc_body(const WgradParams<E>& p, E* sDY, E* sX,
     }
     __syncthreads();  // sX and sDY[buf] are free; sCo holds sample n + G's coefficients
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMA and x loads have landed
-    if (n + p.G < p.N && !WGX(WGX_NO_STAGE) && !WGX(WGX_NO_XLOAD)) put_x();
+    if (n + p.G < p.N) put_x();
     __syncthreads();  // sX and sDY[buf ^ 1] (every wave's DMA) complete
   }
 #pragma unroll
@@ -857,7 +837,9 @@ struct Plan {
   int64_t gn_part, w_part;
 };
 
-Plan make_plan(int n, int h, int w, int cin) {
+// force_c96: mc_conv_wgrad_gn, which only k_wgrad_c96 implements (the forward that skipped the
+// conv1 outputs may have run under another weight-gradient variant: ADVICE r05)
+Plan make_plan(int n, int h, int w, int cin, bool force_c96 = false) {
   Plan pl;
   const int ncu = num_cus();
   pl.grid_d = n < 2 * ncu ? n : 2 * ncu;
@@ -870,7 +852,7 @@ Plan make_plan(int n, int h, int w, int cin) {
   // 16x16 boards, 96 channels, variant 3: k_wgrad_c96, one workgroup (partial row) per CU
   if (cin == 96 && h == 16 && w == 16) {
     if (ncu > gmax) gmax = ncu;
-    pl.c96 = g_variant[MCV_WGRAD] == 0 || g_variant[MCV_WGRAD] == 3;
+    pl.c96 = force_c96 || g_variant[MCV_WGRAD] == 0 || g_variant[MCV_WGRAD] == 3;
     if (pl.c96) pl.G = pl.grid_w = n < ncu ? n : ncu;
   }
   pl.gn_part = (int64_t)pl.grid_d * 3 * COUT;
@@ -979,11 +961,6 @@ int run_wgrad(const Plan& pl, const uint16_t* dy, const uint16_t* x, float* dw, 
   wp.H = h;
   wp.W = w_;
   wp.G = pl.G;
-#ifdef MC_WSX
-  wp.exp = g_wgrad_exp;
-#else
-  wp.exp = 0;
-#endif
   const size_t lds = (size_t)wgrad_lds(h, w_);
   if (pl.c96) {
     if (gn.stats) launch_wgrad_c96<E, true>(wp, pl.grid_w, s);
@@ -1033,10 +1010,6 @@ int run_bwd(const uint16_t* dout, const uint16_t* out, const uint8_t* relu_mask,
 
 extern "C" {
 
-#ifdef MC_WSX
-// timing experiments only (tools/wgrad_exp.py): WGX_* bits of the next k_wgrad launches
-void mc_set_wgrad_exp(int32_t e) { g_wgrad_exp = e; }
-#endif
 
 int64_t mc_conv_gn_bwd_workspace(int32_t n, int32_t h, int32_t w_, int32_t cin) {
   if (n <= 0 || h <= 0 || w_ <= 0 || (cin != 16 && cin != 96)) return -1;
@@ -1074,9 +1047,9 @@ int mc_conv_wgrad_gn(const uint16_t* dy, const uint16_t* y, const float* stats, 
     snprintf(g_err, sizeof g_err, "mc_conv_wgrad_gn: bad argument");
     return MS_EINVAL;
   }
-  const Plan pl = make_plan(n, h, w_, 96);
+  const Plan pl = make_plan(n, h, w_, 96, true);
   if (!pl.c96) {
-    snprintf(g_err, sizeof g_err, "mc_conv_wgrad_gn: needs k_wgrad_c96 (16x16 boards, weight-gradient variant 0 or 3)");
+    snprintf(g_err, sizeof g_err, "mc_conv_wgrad_gn: needs k_wgrad_c96 (16x16 boards with 96 channels)");
     return MS_EINVAL;
   }
   if (work_floats < pl.gn_part + pl.w_part) {

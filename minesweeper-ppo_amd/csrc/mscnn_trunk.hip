@@ -88,7 +88,7 @@ struct TrunkFwdParams {
   TFLayer<E> L[MAXL];
 };
 
-// The value head's global average pool (cnn_residual.py:97-98, AdaptiveAvgPool2d(1)) of the
+// The value head's global average pool (cnn_residual.py:65, AdaptiveAvgPool2d(1)) of the
 // last layer's output tile while it is still in LDS: threads c + 96 h (h = 0, 1) sum channel c
 // over pixel half h on four interleaved f32 accumulators, the halves combine in fixed order
 // through sTmp ([2][96] f32), and the sum is scaled by 1 / P. Every thread of the workgroup
@@ -1816,7 +1816,7 @@ int run_trunk_fwd(const uint16_t* x0, const mc_fwd_layer* layers, int nl, void* 
     if (P == 256) return launch_trunk_fwd2<E, 2, true>(p, s);
     return P <= 128 ? launch_trunk_fwd2<E, 1, false>(p, s) : launch_trunk_fwd2<E, 2, false>(p, s);
   }
-  if (P == 256) return launch_trunk_fwd<E, 2, true>(p, s);
+  // k_trunk_fwd (one sample per 256-thread workgroup): boards of more than 256 cells
   const int npt = ((P + 31) / 32 + WAVES - 1) / WAVES;
   switch (npt) {
     case 1: return launch_trunk_fwd<E, 1, false>(p, s);

@@ -16,8 +16,9 @@ def exact_fp32_convs() -> bool:
     shipped model ~130x further from a float64 computation than the reference's own fp32 CPU
     gradients (tools/grad_diag.py on MI355X); without them the error is <= 2x.
     Sets MIOPEN_DEBUG_CONV_WINOGRAD=0 unless the user chose a value, and logs it once. MIOpen
-    reads it at its first convolution, so the entry points that build or run a model call this
-    (``build_model``, ``Trainer``, ``evaluate_model``); importing ``ms_amd`` does not, so other
+    reads it at its first convolution, so every model constructor of ms_amd.models calls this
+    (a model built directly, as the reference's code builds it, got Winograd), as do
+    ``build_model``, ``Trainer`` and ``evaluate_model``; importing ``ms_amd`` does not, so other
     models in the same process keep MIOpen's defaults unless one of those ran first (the setting
     is process-wide). The 16-bit training path runs the fused kernels and never
     reaches MIOpen. Returns True when the setting is in effect."""

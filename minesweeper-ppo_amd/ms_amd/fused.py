@@ -688,7 +688,7 @@ def heads_apply(f: torch.Tensor, pol, mine=None, pooled: Optional[torch.Tensor] 
 
 
 # ------------------------------------------------------------------------------------
-# The value head's MLP (cnn_residual.py:97-102: Linear 96 -> H, ReLU, Linear H -> H, ReLU,
+# The value head's MLP (cnn_residual.py:64-72: Linear 96 -> H, ReLU, Linear H -> H, ReLU,
 # Linear H -> 1) on the pooled features under 16-bit autocast.
 
 VALUE_SPLITK = 32  # row chunks of the weight gradients' batched GEMMs; 0: autocast's nn.Linear chain

@@ -25,6 +25,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import exact_fp32_convs
+
 
 class GroupNorm(nn.GroupNorm):
     """nn.GroupNorm with the affine step done as plain elementwise ops.
@@ -85,6 +87,7 @@ class CNNResidualPolicy(nn.Module):
     def __init__(self, in_channels: int, *, stem_channels: int = 128, blocks: int = 6,
                  dropout: float = 0.05, value_hidden: int = 256) -> None:
         super().__init__()
+        exact_fp32_convs()  # fp32 3x3 convolutions without MIOpen's Winograd (ms_amd.exact_fp32_convs)
         if stem_channels <= 0:
             raise ValueError("stem_channels must be positive")
         if blocks <= 0:
@@ -181,6 +184,7 @@ class CNNPolicy(nn.Module):
 
     def __init__(self, in_channels: int, hidden: int = 64) -> None:
         super().__init__()
+        exact_fp32_convs()  # fp32 3x3 convolutions without MIOpen's Winograd (ms_amd.exact_fp32_convs)
         hidden = int(hidden)
         if hidden <= 0:
             raise ValueError("hidden must be positive")

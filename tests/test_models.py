@@ -110,3 +110,14 @@ def test_models_take_cell_codes_on_cpu():
             b = m(codes_to_obs(codes), return_mine=True)
         for x, y in zip(a, b):
             assert torch.equal(x, y), name
+
+
+def test_model_constructors_select_exact_fp32_convs(monkeypatch):
+    """Building CNNResidualPolicy / CNNPolicy directly (as the reference's code does, without
+    build_model) turns MIOpen's fp32 Winograd convolutions off too."""
+    from ms_amd.models import CNNPolicy, CNNResidualPolicy
+    for ctor in (lambda: CNNResidualPolicy(10, stem_channels=16, blocks=1, value_hidden=8), lambda: CNNPolicy(10)):
+        monkeypatch.delenv("MIOPEN_DEBUG_CONV_WINOGRAD", raising=False)
+        ctor()
+        import os
+        assert os.environ.get("MIOPEN_DEBUG_CONV_WINOGRAD") == "0"

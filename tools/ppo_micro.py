@@ -23,6 +23,7 @@ ap.add_argument("--pure-bf16", action="store_true", help="model + obs in bf16, n
 ap.add_argument("--no-wgrad-gn", action="store_true", help="write conv1 outputs instead of recomputing them")
 ap.add_argument("--value-splitk", type=int, default=32, help="fused.VALUE_SPLITK (0: autocast's Linear chain)")
 ap.add_argument("--torch-prof", type=int, default=0, help="print the device time of N minibatches by aten op")
+ap.add_argument("--foreach-adamw", action="store_true", help="torch's foreach AdamW instead of the fused kernel")
 args = ap.parse_args()
 torch.backends.cudnn.benchmark = args.benchmark
 from ms_amd import fused as _F  # noqa: E402
@@ -41,7 +42,7 @@ if args.pure_bf16:
     m = m.to(torch.bfloat16)
 if args.channels_last:
     m = m.to(memory_format=torch.channels_last)
-opt = torch.optim.AdamW(m.parameters(), lr=3e-4)
+opt = torch.optim.AdamW(m.parameters(), lr=3e-4, fused=not args.foreach_adamw)  # as the Trainer
 M = args.mb
 g = torch.Generator(device=dev).manual_seed(0)
 rev = torch.rand(M, 16, 16, device=dev, generator=g) < 0.4

@@ -182,7 +182,8 @@ class Trainer:
         # the reference's AdamW (train_rl.py:415, default weight decay) as ONE fused kernel on the GPU:
         # the same update per element; under GradScaler the found-inf skip stays on the device (the
         # foreach path's step() reads found_inf on the host, a sync per minibatch) -- DESIGN.md §8
-        self.opt = AdamW(self.model.parameters(), lr=cfg.lr, fused=self.device.type == "cuda")
+        fused = self.device.type == "cuda" and os.environ.get("MS_FOREACH_ADAMW", "0") == "0"  # (A/B knob)
+        self.opt = AdamW(self.model.parameters(), lr=cfg.lr, fused=fused)
         self.sched = CosineAnnealingLR(self.opt, T_max=cfg.total_updates)
         self.amp_dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": None}[amp]
         self.scaler = torch.amp.GradScaler("cuda") if amp == "fp16" else None

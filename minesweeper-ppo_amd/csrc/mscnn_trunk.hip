@@ -1053,32 +1053,32 @@ __global__ __launch_bounds__(512, 1) void k_trunk_fwd_pp(TrunkFwdParams<E> p) {
       const float inv_cnt = 1.0f / (16.0f * (float)P);
       // ---- P0: GroupNorm sums; the residual, the GN parameters, the next sample's input in flight ----
       pp_wait_vm<0>();  // weight pieces this wave issued at its last tap (the MFMA team's tap 0 needs them)
-      // the residual (block input) of a conv2 layer: piece q's 4 x 8 B, loaded two pieces ahead (P0
-      // loads pieces 0 and 1) into a 3-deep register ring, always before the stores they pass
+      // the residual (block input) of a conv2 layer: gathered at P0 by LDS-DMA into this wave's own
+      // pixel rows of the tile (the taps have read them; coalesced 16-B chunks), read back per piece
+      // as 8-byte pieces in the accumulators' layout (each lane then overwrites what it read)
       const E* res = nullptr;
-      u32x2 rv[3][4];
-      auto load_res = [&](int q) {
-        const PPLane ln = pp_lane();
-        const int t = q % NPT, ct = q / NPT;
-        const int px = (wave * NPT + t) * 32 + ln.l32;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          rv[q % 3][g] = u32x2{0u, 0u};
-          if (res && (FULL || px < P))
-            rv[q % 3][g] = *reinterpret_cast<const u32x2*>(res + (size_t)px * COUT + ct * 32 + 8 * g + 4 * ln.hh);
-        }
-      };
       float gmv = 0.f, btv = 0.f, dmv = 1.f;
       {
         const PPLane ln = pp_lane();
         if (act) {
-          if (last && k + 1 < nS) issue_x0(sample_of(k + 1), ln.lane);
           if (l & 1) res = l == 1 ? p.x0 + so : (p.L[l - 2].out ? p.L[l - 2].out + so : p.ws + ((size_t)blockIdx.x * 2 + team) * P * COUT);
 #ifdef MC_DIAG
           if (p.dflags & 2) res = nullptr;
 #endif
-          load_res(0);
-          load_res(1);
+          if (res) {
+#pragma unroll
+            for (int t = 0; t < NPT; ++t) {
+              const int r0 = (wave * NPT + t) * 32;
+#pragma unroll
+              for (int kk = 0; kk < 6; ++kk) {
+                const int qb = r0 * PPRS + kk * 1024 + ln.lane * 16;
+                if (qb < P * PPRS) {
+                  const int r = qb / PPRS, cs = (qb - r * PPRS) >> 4;
+                  pp_dma(res, (uint32_t)(r * PPRS + ((cs ^ ((r >> 2) & 3)) << 4)), tile0 + r0 * PPRS + kk * 1024);
+                }
+              }
+            }
+          }
           if (ln.ttid < COUT) {
             gmv = p.L[l].gamma[ln.ttid];
             btv = p.L[l].beta[ln.ttid];
@@ -1180,27 +1180,37 @@ __global__ __launch_bounds__(512, 1) void k_trunk_fwd_pp(TrunkFwdParams<E> p) {
         }
 #endif
       }
-      uint32_t rw[NPT][3];
+      // the next sample's input, gathered by LDS-DMA into this wave's own pixel rows once its last
+      // pixel tile is staged (the epilogue stages y / out through those rows)
+      const bool x0next = act && last && k + 1 < nS;
       // the pieces, specialised on the value head's pool (the last layer only)
       auto pieces = [&](auto POOL) {
       constexpr bool pool = decltype(POOL)::value;
-      float pl[16];
+      uint32_t rw[3];      // ReLU bits of the current pixel tile, per channel tile
+      u32x2 ohold[3][4];   // SAVE: the tile's outputs wait here while y passes through its rows
 #pragma unroll
       for (int q = 0; q < 6; ++q) {
         if (q < 3 * NPT && act) {
-          const int ct = q / NPT, t = q % NPT;
-          if (q + 2 < 3 * NPT) load_res(q + 2);
+          const int t = q / 3, ct = q % 3;  // pixel tile t, channel tile ct
           const PPLane ln = pp_lane();
           const int px = (wave * NPT + t) * 32 + ln.l32;
           const bool pv = FULL || px < P;
           uint32_t word = 0u;
+          float pl[16];
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             const int co = ct * 32 + 8 * g + 4 * ln.hh;
             const f32x4 ca = *reinterpret_cast<const f32x4*>(&sAB[co]);
             const f32x4 cb = *reinterpret_cast<const f32x4*>(&sAB[COUT + co]);
             const f32x4 cd = *reinterpret_cast<const f32x4*>(&sAB[2 * COUT + co]);
-            const E4 rh = __builtin_bit_cast(E4, rv[q % 3][g]);
+            // this lane's 8 bytes of pixel px, chunk ct * 4 + g: the residual (conv2) in, then y
+            // (SAVE: staged for the coalesced store below, the output kept in registers meanwhile)
+            // or the output itself out
+            unsigned char* slot = sTile + pp_swz(px, ct * 4 + g) + ln.hh * 8;
+            E4 rh;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) rh[e] = (E)0.f;
+            if (res && pv) rh = *reinterpret_cast<const E4*>(slot);
             E4 yh, oh;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -1212,22 +1222,15 @@ __global__ __launch_bounds__(512, 1) void k_trunk_fwd_pp(TrunkFwdParams<E> p) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) nib |= ((float)oh[e] > 0.f ? 1u : 0u) << e;
             word |= nib << (8 * g + 4 * ln.hh);
-            const size_t go = (size_t)px * COUT + co;
-            if (pv) {
-              if (SAVE) *reinterpret_cast<u32x2*>(ysave + go) = __builtin_bit_cast(u32x2, yh);
-              if (!last) *reinterpret_cast<u32x2*>(sTile + pp_swz(px, ct * 4 + g) + ln.hh * 8) = __builtin_bit_cast(u32x2, oh);
-              if (out) *reinterpret_cast<u32x2*>(out + go) = __builtin_bit_cast(u32x2, oh);
-            }
+            if (SAVE) ohold[ct][g] = __builtin_bit_cast(u32x2, oh);
+            if (pv) *reinterpret_cast<u32x2*>(slot) = __builtin_bit_cast(u32x2, SAVE ? yh : oh);
             if (pool) {
 #pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const float o = pv ? (float)oh[e] : 0.f;
-                pl[4 * g + e] = t == 0 ? o : pl[4 * g + e] + o;
-              }
+              for (int e = 0; e < 4; ++e) pl[4 * g + e] = pv ? (float)oh[e] : 0.f;
             }
           }
-          rw[t][ct] = word;
-          if (pool && t == NPT - 1) {  // this channel tile's sums over the wave's pixels -> sPool (lanes 31, 63)
+          rw[ct] = word;
+          if (pool) {  // this piece's sums over the wave's pixels -> sPool (lanes 31, 63; tile 1 adds)
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
               float v = row_sum16(pl[i]);
@@ -1236,28 +1239,60 @@ __global__ __launch_bounds__(512, 1) void k_trunk_fwd_pp(TrunkFwdParams<E> p) {
             }
             if (ln.l32 == 31) {
 #pragma unroll
-              for (int g = 0; g < 4; ++g)
-                *reinterpret_cast<f32x4*>(&sPool[wave * COUT + ct * 32 + 8 * g + 4 * ln.hh]) =
-                    f32x4{pl[4 * g], pl[4 * g + 1], pl[4 * g + 2], pl[4 * g + 3]};
+              for (int g = 0; g < 4; ++g) {
+                f32x4* sp = reinterpret_cast<f32x4*>(&sPool[wave * COUT + ct * 32 + 8 * g + 4 * ln.hh]);
+                const f32x4 v4{pl[4 * g], pl[4 * g + 1], pl[4 * g + 2], pl[4 * g + 3]};
+                *sp = t == 0 ? v4 : *sp + v4;
+              }
+            }
+          }
+          if (ct == 2) {
+            // pixel tile t complete. Its 32 rows (6 KiB, contiguous in the tile) leave as 16-B chunks
+            // in row order -- one 1-KiB coalesced store per wave instruction -- instead of 8-B
+            // pieces at 192-B strides: y first (SAVE), then the outputs (block outputs / residual slot)
+            const int r0 = (wave * NPT + t) * 32;
+            auto flush = [&](E* dst) {
+#pragma unroll
+              for (int kk = 0; kk < 6; ++kk) {
+                const int gi = kk * 64 + ln.lane, r = r0 + gi / 12, c = gi - (gi / 12) * 12;
+                const u32x4 v = *reinterpret_cast<const u32x4*>(sTile + pp_swz(r, c));
+                if (FULL || r < P) *reinterpret_cast<u32x4*>(dst + (size_t)r * COUT + c * 8) = v;
+              }
+            };
+            if (SAVE) {
+              flush(ysave);
+#pragma unroll
+              for (int c2 = 0; c2 < 3; ++c2)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                  if (pv) *reinterpret_cast<u32x2*>(sTile + pp_swz(px, c2 * 4 + g) + ln.hh * 8) = ohold[c2][g];
+            }
+            if (out) flush(out);
+            if (SAVE) {  // ReLU bits: byte ct * 4 + g = low nibble (hh 0) | high nibble (hh 1)
+              uint32_t b3[3];
+#pragma unroll
+              for (int c2 = 0; c2 < 3; ++c2) b3[c2] = rw[c2] | (uint32_t)__shfl_xor((int)rw[c2], 32);
+              if (ln.hh == 0 && pv) {
+                uint32_t* rp = reinterpret_cast<uint32_t*>(rmask + (size_t)px * C8);
+                rp[0] = b3[0];
+                rp[1] = b3[1];
+                rp[2] = b3[2];
+              }
+            }
+            if (x0next) {  // this wave's rows of the next sample's input (all its reads of them done)
+              const E* src = p.x0 + (size_t)sample_of(k + 1) * P * COUT;
+#pragma unroll
+              for (int kk = 0; kk < 6; ++kk) {
+                const int qb = (r0 * PPRS) + kk * 1024 + ln.lane * 16;
+                if (qb < P * PPRS) {
+                  const int r = qb / PPRS, cs = (qb - r * PPRS) >> 4;
+                  pp_dma(src, (uint32_t)(r * PPRS + ((cs ^ ((r >> 2) & 3)) << 4)), tile0 + r0 * PPRS + kk * 1024);
+                }
+              }
             }
           }
         }
-        if (q == 5 && act && SAVE) {  // ReLU bits: byte ct * 4 + g = low nibble (hh 0) | high nibble (hh 1)
-          const PPLane ln = pp_lane();
-#pragma unroll
-          for (int t = 0; t < NPT; ++t) {
-            const int px = (wave * NPT + t) * 32 + ln.l32;
-            uint32_t b3[3];
-#pragma unroll
-            for (int ct = 0; ct < 3; ++ct) b3[ct] = rw[t][ct] | (uint32_t)__shfl_xor((int)rw[t][ct], 32);
-            if (ln.hh == 0 && (FULL || px < P)) {
-              uint32_t* rp = reinterpret_cast<uint32_t*>(rmask + (size_t)px * C8);
-              rp[0] = b3[0];
-              rp[1] = b3[1];
-              rp[2] = b3[2];
-            }
-          }
-        }
+        if (q == 5 && x0next) pp_wait_vm<0>();  // the next sample's input has landed (its taps follow)
         if (q == 5 && pool && act) pool_n = n;
         TSTAMP(4);
 #ifdef MC_DIAG

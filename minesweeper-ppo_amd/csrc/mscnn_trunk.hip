@@ -21,8 +21,10 @@
 //                sums; pass 2: dy to LDS and to HBM for the weight gradient), then the data
 //                gradient dx = sum_tap shift(dy) . W^T on the MFMA, staged in LDS where the
 //                NEXT layer's pass 1 reads it as its dout. The skip gradient of a block (dz of
-//                its conv2) waits in a per-workgroup slot of the workspace for two layers and
-//                is added where the block input's gradient is formed. The stem's GroupNorm
+//                its conv2) is added where the block input's gradient is formed, two layers
+//                later: it waits in registers (boards of <= 256 cells: each lane keeps the 48
+//                channels of its pixels that it writes as dx) or in a per-workgroup slot of
+//                the workspace (larger boards, no registers to spare). The stem's GroupNorm
 //                backward closes the chain (its input needs no gradient). d gamma / d beta /
 //                d bias per layer accumulate per workgroup (fixed sample order) and are summed
 //                over workgroups by k_reduce: deterministic.
@@ -1378,6 +1380,12 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_bwd(TrunkBwdPar
   float* sTmp = sCo + 3 * COUT;                                                       // [2][96]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, l32 = lane & 31, hh = lane >> 5;
   const float inv_cnt = 1.0f / (16.0f * (float)P);
+  // HOLD: the skip gradient dz of a conv2 stays in registers until the dx of the block's conv1
+  // (the next layer down) is written, in the dx lane layout: pixel (wave NPT + t) 32 + l32,
+  // channels ct 32 + 8 g + 4 hh + 0..3 -- 4 x 16-bit each, 48 VGPRs at NPT = 2. Otherwise it
+  // makes a round trip through the workgroup's workspace slot (L2 / Infinity Cache)
+  constexpr bool HOLD = NPT <= 2;
+  u32x2 zk[HOLD ? NPT : 1][3][4];
 
   for (int i = threadIdx.x; i < DCP / 8; i += 256) *reinterpret_cast<u32x4*>(&sD[P * DCP + 8 * i]) = u32x4{0u, 0u, 0u, 0u};
   int qr[NPT], qc[NPT];
@@ -1410,8 +1418,9 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_bwd(TrunkBwdPar
       const bool gact = tid < PG * C8;
       const int grp = c8 >> 1;
       const bool top = li == p.NL - 1;
-      const bool addd = !(li & 1) && li + 2 < p.NL;  // dout += the skip gradient dz_{li+2}
-      const bool keep_dz = !(li & 1) && li >= 2;     // dz of a conv2: the skip gradient of layer li-2
+      const bool addd = !HOLD && !(li & 1) && li + 2 < p.NL;  // dout += the skip gradient dz_{li+2}
+      const bool keep_dz = !(li & 1) && li >= 2;              // dz of a conv2: the skip gradient of layer li-2
+      const bool addz = HOLD && (li & 1) && li + 1 < p.NL;    // dx += the held dz_{li+1} (layer li-1's dout)
       float* pp = p.part + ((size_t)vb * p.NL + li) * 3 * COUT;
       float acc_g = 0.f, acc_b = 0.f, acc_bias = 0.f;  // tid < 96: this partial row's running sums
       if (tid < COUT && n != vb) {
@@ -1513,6 +1522,18 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_bwd(TrunkBwdPar
         }
       }
       __syncthreads();
+      if (HOLD && keep_dz) {  // dz is complete in the tile; pass 2 overwrites it two barriers on
+#pragma unroll
+        for (int t = 0; t < (HOLD ? NPT : 1); ++t) {
+          const int px = (wave * NPT + t) * 32 + l32;
+          if (px < P) {
+#pragma unroll
+            for (int ct = 0; ct < 3; ++ct)
+#pragma unroll
+              for (int g = 0; g < 4; ++g) zk[t][ct][g] = *reinterpret_cast<const u32x2*>(&sD[px * DCP + ct * 32 + 8 * g + 4 * hh]);
+          }
+        }
+      }
       float S1 = 0.f, S2 = 0.f, S3 = 0.f, gam = 0.f, cmean = 0.f, crstd = 0.f;
       if (tid < COUT) {
         for (int g = 0; g < PG; ++g) {
@@ -1574,9 +1595,9 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_bwd(TrunkBwdPar
             E* sp = &sD[px * DCP + c8 * 8];
             const u32x4 zv = *reinterpret_cast<const u32x4*>(sp);
 #ifdef MC_DIAG
-            if (keep_dz && !(p.dflags & 1)) *reinterpret_cast<u32x4*>(&wsl[(size_t)px * COUT + c8 * 8]) = zv;
+            if (!HOLD && keep_dz && !(p.dflags & 1)) *reinterpret_cast<u32x4*>(&wsl[(size_t)px * COUT + c8 * 8]) = zv;
 #else
-            if (keep_dz) *reinterpret_cast<u32x4*>(&wsl[(size_t)px * COUT + c8 * 8]) = zv;
+            if (!HOLD && keep_dz) *reinterpret_cast<u32x4*>(&wsl[(size_t)px * COUT + c8 * 8]) = zv;
 #endif
             const E8 z8 = __builtin_bit_cast(E8, zv);
             const E8 y8 = __builtin_bit_cast(E8, yr[i]);
@@ -1670,7 +1691,8 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_bwd(TrunkBwdPar
       }
       TSTAMP(3);
       // dx -> the tile (16-bit, as the per-layer kernel's dx store): layer li-1's dout; lane = pixel,
-      // channels ct * 32 + 8 g + 4 hh + 0..3 as one 8-byte write
+      // channels ct * 32 + 8 g + 4 hh + 0..3 as one 8-byte write. addz: + the held skip gradient,
+      // rounded as pass 1's addend path (the per-layer kernel's dx (+ addend) store)
 #pragma unroll
       for (int t = 0; t < NPT; ++t) {
         const int px = (wave * NPT + t) * 32 + l32;
@@ -1682,6 +1704,11 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_bwd(TrunkBwdPar
               typename EV<E>::v4 d4;
 #pragma unroll
               for (int e = 0; e < 4; ++e) d4[e] = (E)acc[t][ct][4 * g + e];
+              if (addz) {
+                const typename EV<E>::v4 z4 = __builtin_bit_cast(typename EV<E>::v4, zk[HOLD ? t : 0][ct][g]);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) d4[e] = (E)pin_f32((float)d4[e] + (float)z4[e]);
+              }
               *reinterpret_cast<u32x2*>(&sD[px * DCP + ct * 32 + 8 * g + 4 * hh]) = __builtin_bit_cast(u32x2, d4);
             }
         }

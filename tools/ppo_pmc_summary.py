@@ -102,6 +102,9 @@ for k, ds in dur.items():
            "fetch_doubled": wide}
     if k in mb and gui.get(k):
         rec["mfma_busy_frac"] = mb[k] / (gui[k] / 8.0 * 1024.0)
+        # GRBM_GUI_ACTIVE counts shader-clock cycles per XCD: over the traced duration, the kernel's
+        # mean engine clock (MI355X peak 2.4 GHz; the MFMA peak scales with it)
+        rec["sclk_GHz"] = gui[k] / 8.0 / (us * 1e3)
     nl = a.trunk_layers if k.startswith("k_trunk") else (1 if layer96(k) else 0)
     if nl:  # a k_trunk_* launch runs every 96->96 layer of the stack (the backward's stem has no dgrad)
         rec["layers96"] = nl
@@ -112,4 +115,4 @@ for k, ds in dur.items():
 json.dump({"samples": a.samples, "kernels": rows}, open(a.out, "w"), indent=1)
 for k, r in sorted(rows.items(), key=lambda kv: -kv[1]["mean_us"] * kv[1]["launches"]):
     print(f"{r['mean_us']:9.1f} us x{r['launches']:3d} traffic {r['traffic_bytes'] / 1e9:6.2f} GB "
-          f"mfma_busy {r.get('mfma_busy_frac', float('nan')):.3f} {k[:90]}")
+          f"mfma_busy {r.get('mfma_busy_frac', float('nan')):.3f} sclk {r.get('sclk_GHz', float('nan')):.2f} GHz {k[:90]}")

@@ -25,6 +25,7 @@ import torch
 import torch.distributed as dist
 import torch.nn.functional as F
 
+from . import loss as _loss
 from .profiling import prange
 
 
@@ -126,6 +127,9 @@ def ppo_losses(model, batch, cfg: PPOConfig, amp_dtype: Optional[torch.dtype] = 
         else:
             logits, value = model(batch.obs, return_mine=False)
             mine_logits = None
+        if logits.is_cuda and _loss.FUSED_LOSS and logits.shape[-1] <= 512:
+            return _fused_losses(model, batch, cfg, amp_dtype, group, world, logits, value,
+                                 mine_logits if need_mine else None)
         neg_inf = -1e4 if logits.dtype in (torch.float16, torch.bfloat16) else -1e9
         masked = logits.masked_fill(~batch.action_mask, neg_inf)
         logp = F.log_softmax(masked, dim=-1)
@@ -171,6 +175,33 @@ def ppo_losses(model, batch, cfg: PPOConfig, amp_dtype: Optional[torch.dtype] = 
         if cfg.beta_l2 > 0 and hasattr(model, "beta_regularizer"):
             loss = loss + cfg.beta_l2 * model.beta_regularizer()
         out["loss"] = loss
+    return out
+
+
+def _fused_losses(model, batch, cfg, amp_dtype, group, world, logits, value, mine_logits):
+    """ppo_losses' terms from csrc/msppo.hip (ms_amd/loss.py): the same quantities, roundings
+    and global belief counts, in one HIP pass forward and one backward (ppo.py:33-87)."""
+    ml = mine_logits if (mine_logits is not None and getattr(batch, "mine_labels", None) is not None) else None
+    counts = None
+    if ml is not None:
+        y = batch.mine_labels
+        vmask = getattr(batch, "mine_valid", None)
+        vm = torch.ones_like(y) if vmask is None else vmask.to(y.dtype)
+        counts = torch.stack([(y * vm).sum(), vm.sum()])
+        if group is not None:
+            dist.all_reduce(counts, group=group)
+    amp16 = amp_dtype if (batch.obs.is_cuda and amp_dtype in (torch.float16, torch.bfloat16)) else None
+    t = _loss.ppo_loss_terms(logits, value, ml, batch, cfg, counts, world, amp16)
+    out = {"policy_loss": t[0], "value_loss": t[1], "entropy": t[2]}
+    if ml is not None:
+        if cfg.aux_mine_weight > 0:
+            out["aux_bce"] = t[3]
+        if cfg.aux_mine_calib_weight > 0:
+            out["aux_calib"] = t[4]
+    loss = t[5]
+    if cfg.beta_l2 > 0 and hasattr(model, "beta_regularizer"):
+        loss = loss + cfg.beta_l2 * model.beta_regularizer()
+    out["loss"] = loss
     return out
 
 

@@ -46,6 +46,22 @@ def test_library_exports_every_cnn_header_symbol():
         assert hasattr(lib, name), name
 
 
+def test_library_exports_every_ppo_loss_header_symbol():
+    from ms_amd import _lib as L
+    lib = L.load()
+    fns = header_functions([os.path.join(ROOT, "include", "msppo.h")], "mc_")
+    assert {"mc_ppo_loss_workspace", "mc_ppo_loss_fwd", "mc_ppo_loss_bwd"} <= set(fns)
+    for name in fns:
+        assert hasattr(lib, name), name
+    # ms_amd/loss.py's ctypes mirror of mc_ppo_loss_args has the C layout (12 pointers, 2 int32,
+    # 8 floats, int64, int32 -> 152 bytes)
+    from ms_amd.loss import _Args
+    assert ctypes.sizeof(_Args) == 152 and _Args.M.offset == 136 and _Args.A.offset == 144
+    ws = lib.mc_ppo_loss_workspace
+    ws.restype, ws.argtypes = ctypes.c_int64, [ctypes.c_int64]
+    assert ws(0) == -1 and ws(32768) == 2048 * 8 + 32768 * 4
+
+
 def test_cnn_entry_points_validate_arguments():
     from ms_amd import _lib as L
     lib = L.load()

@@ -247,6 +247,35 @@ def _packed(w: torch.Tensor, kind: str, dtype: torch.dtype, cin_pad: int = 0) ->
     return t
 
 
+def _packed_many(ws, kind: str, dtype: torch.dtype) -> list:
+    """``_packed`` of a list of 96 -> 96 conv weights: the stale ones re-laid out together, one
+    stack and one permuting cast for all of them (two launches a minibatch instead of two per
+    layer; the values are the per-layer re-layout's, element for element)."""
+    out, stale = [None] * len(ws), []
+    for i, w in enumerate(ws):
+        ent = _wcache.get(w)
+        hit = ent.get((kind, dtype)) if ent is not None else None
+        if hit is not None and hit[0] == w._version:
+            out[i] = hit[1]
+        else:
+            stale.append(i)
+    if len(stale) == 1:
+        out[stale[0]] = _packed(ws[stale[0]], kind, dtype, COUT)
+    elif stale:
+        src = torch.stack([ws[i].detach() for i in stale])  # [S, co, ci, 3, 3]
+        assert src.shape[1:] == (COUT, COUT, 3, 3)
+        dst = torch.empty((len(stale), 3, 3, COUT, COUT), dtype=dtype, device=src.device)
+        dst.copy_(src.permute(0, 3, 4, 1, 2) if kind == "f" else src.permute(0, 3, 4, 2, 1))
+        dst = dst.view(len(stale), 9, COUT, COUT)
+        for j, i in enumerate(stale):
+            ent = _wcache.get(ws[i])
+            if ent is None:
+                ent = _wcache[ws[i]] = {}
+            out[i] = dst[j]
+            ent[(kind, dtype)] = (ws[i]._version, out[i])
+    return out
+
+
 def trunk_layers(model) -> list:
     """[(conv, norm)] in execution order: stem, then (conv1, norm1), (conv2, norm2) per block."""
     layers = [(model.stem[0], model.stem[1])]
@@ -339,6 +368,7 @@ def trunk_forward_chain(x, layers, H: int, W: int, dmasks, save: bool, pooled: O
     keep = []  # f32 parameter copies must outlive the enqueue (the allocator may reuse their memory only after)
     outs, ys, sts, rms = [], [], [], []
     eps = res[0][1].eps
+    wts = _packed_many([conv.weight for conv, _ in res], "f", et)
     for k, (conv, norm) in enumerate(res):
         assert norm.eps == eps and conv.weight.shape[0] == COUT and conv.weight.shape[1] == COUT
         f32c = lambda t: t.detach().to(torch.float32).contiguous()  # noqa: E731
@@ -359,7 +389,7 @@ def trunk_forward_chain(x, layers, H: int, W: int, dmasks, save: bool, pooled: O
             ys.append(y)
             sts.append(st)
             rms.append(rm)
-        arr[k] = _FwdLayer(L.ptr(_packed(conv.weight, "f", et, COUT)), L.ptr(b), L.ptr(g), L.ptr(be), L.ptr(dm),
+        arr[k] = _FwdLayer(L.ptr(wts[k]), L.ptr(b), L.ptr(g), L.ptr(be), L.ptr(dm),
                            L.ptr(out), L.ptr(y), L.ptr(st), L.ptr(rm))
         if last:
             final = out
@@ -382,12 +412,13 @@ def trunk_backward_chain(dout, layers, ys, sts, rms, dmasks, H: int, W: int):
     nl = len(layers)
     arr = (_BwdLayer * nl)()
     keep, dys = [], []
+    wTs = [None] + _packed_many([conv.weight for conv, _ in layers[1:]], "t", et)
     for li, (conv, norm) in enumerate(layers):
         g = norm.weight.detach().to(torch.float32).contiguous()
         dm = None
         if li % 2 == 1 and dmasks is not None:
             dm = dmasks[(li - 1) // 2].to(torch.float32).contiguous()
-        wT = _packed(conv.weight, "t", et) if li > 0 else None
+        wT = wTs[li]
         dy = torch.empty((n, p, COUT), dtype=et, device=dev)
         keep += [g, dm]
         dys.append(dy)

@@ -30,7 +30,8 @@ def _outputs(M, A, dev, vdt, seed):
     mine = (torch.randn(M, 1, A, generator=g) * 2).to(dev)
     labels = (torch.rand(M, A, generator=g) < 0.15).float()
     valid = torch.rand(M, A, generator=g) < 0.6
-    valid[1] = False  # a row with no valid cell
+    if M > 1:
+        valid[1] = False  # a row with no valid cell
     # old log-probs near the current ones: ratios on both sides of the clip range
     with torch.no_grad():
         lp = torch.log_softmax(logits.cpu().masked_fill(~mask, -1e9), -1)[torch.arange(M), actions]
@@ -110,6 +111,48 @@ def test_fused_loss_deterministic(gpu):
     assert a[0] == b[0]
     for x, y in zip(a[1:], b[1:]):
         assert torch.equal(x, y)
+
+
+def _torch_terms(logits, value, mine, b, cfg, world, counts):
+    """ppo.py:33-87 in f64 from the same inputs (the data-parallel belief scale world / count)."""
+    x = logits.double().masked_fill(~b.action_mask, -1e9)
+    lp = torch.log_softmax(x, -1)
+    r = (lp.gather(1, b.actions.view(-1, 1)).squeeze(1) - b.old_logp.double()).exp()
+    A = b.advantages.double()
+    pol = -torch.min(r * A, r.clamp(1 - cfg.clip_eps, 1 + cfg.clip_eps) * A).mean()
+    v, V, R = value.double().view(-1), b.values.double(), b.returns.double()
+    vc = V + (v - V).clamp(-cfg.clip_eps_v, cfg.clip_eps_v)
+    val = 0.5 * torch.max((v - R) ** 2, (vc - R) ** 2).mean()
+    ent = -(lp.exp() * lp).sum(-1).mean()
+    lf, y = mine.double().reshape(b.mine_labels.shape), b.mine_labels.double()
+    vm = torch.ones_like(y) if getattr(b, "mine_valid", None) is None else b.mine_valid.double()
+    pos, cnt = counts[0].double(), counts[1].double()
+    pw = (cnt - pos + 1e-6) / (pos + 1e-6)
+    scale = world / cnt.clamp_min(1.0)
+    bce = (torch.nn.functional.binary_cross_entropy_with_logits(lf, y, pos_weight=pw, reduction="none") * vm).sum() * scale
+    cal = (((torch.sigmoid(lf) - y) ** 2) * vm).sum() * scale
+    return [pol, val, ent, bce, cal]
+
+
+@pytest.mark.parametrize("M,A,world,valid", [(1, 1, 1, False), (3, 5, 2, True), (517, 81, 4, False), (64, 512, 2, True)],
+                         ids=["1x1", "3x5-world2", "517x81-world4-novalid", "64x512-world2"])
+def test_fused_loss_edge_shapes_and_world(gpu, M, A, world, valid):
+    """Odd shapes (one row, one action, the 512-cell maximum), no valid mask, and the data-parallel
+    belief scale world / global count, against an f64 restatement: terms rel 1e-5."""
+    from ms_amd.loss import ppo_loss_terms
+    from ms_amd.ppo import PPOConfig
+    cfg = PPOConfig(ent_coef=0.003, aux_mine_weight=0.05, aux_mine_calib_weight=0.01)
+    logits, value, mine, b = _outputs(M, A, gpu, torch.float32, seed=M + A)
+    if not valid:
+        b.mine_valid = None
+    vm = torch.ones_like(b.mine_labels) if b.mine_valid is None else b.mine_valid.float()
+    counts = torch.stack([(b.mine_labels * vm).sum(), vm.sum()]) * 1.5  # a "global" count (other ranks)
+    t = ppo_loss_terms(logits, value, mine, b, cfg, counts, world, None)
+    ref = _torch_terms(logits, value, mine, b, cfg, world, counts)
+    for k in range(5):
+        assert float(t[k]) == pytest.approx(float(ref[k]), rel=1e-5, abs=1e-6), k
+    w = [1.0, cfg.vf_coef, -cfg.ent_coef, cfg.aux_mine_weight, cfg.aux_mine_calib_weight]
+    assert float(t[5]) == pytest.approx(sum(wk * float(rk) for wk, rk in zip(w, ref)), rel=1e-5, abs=1e-6)
 
 
 def test_ppo_loss_c_api_rejects_bad_arguments(gpu):

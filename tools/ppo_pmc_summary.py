@@ -104,7 +104,9 @@ for k, ds in dur.items():
         rec["mfma_busy_frac"] = mb[k] / (gui[k] / 8.0 * 1024.0)
         # GRBM_GUI_ACTIVE counts shader-clock cycles per XCD: over the traced duration, the kernel's
         # mean engine clock (MI355X peak 2.4 GHz; the MFMA peak scales with it)
-        rec["sclk_GHz"] = gui[k] / 8.0 / (us * 1e3)
+        # (short kernels excluded: GRBM_GUI_ACTIVE also counts the dispatch's ramp and drain)
+        if us >= 200.0:
+            rec["sclk_GHz"] = gui[k] / 8.0 / (us * 1e3)
     nl = a.trunk_layers if k.startswith("k_trunk") else (1 if layer96(k) else 0)
     if nl:  # a k_trunk_* launch runs every 96->96 layer of the stack (the backward's stem has no dgrad)
         rec["layers96"] = nl

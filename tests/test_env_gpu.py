@@ -55,8 +55,10 @@ def test_trajectory_golden_gpu(gpu, name):
         assert np.array_equal(v.late_rng_state(), z["late_state"])
 
 
-def _diff_run(H, W, K, N, T, mode, seed=0, check_every=1, labels=True, late=None):
+def _diff_run(H, W, K, N, T, mode, seed=0, check_every=1, labels=True, late=None, dbg=0):
     v = _vec(H, W, K, N, seed=seed, late_start_cfg=late, late_start_seed=seed + 1 if late else None)
+    if dbg:
+        v.set_debug_flags(dbg)
     o = O.OracleVec(H, W, K, N, seed=seed, late_start=late, late_seed=seed + 1 if late else None)
     d = v.reset()
     oo, om = o.reset()
@@ -333,6 +335,16 @@ def test_packed16_step_equals_one_board_per_wave(gpu, K, N, mode):
     sa, sb = a.snapshot_tensors(), b.snapshot_tensors()
     for k in sa:
         assert torch.equal(sa[k], sb[k]), k
+
+
+@pytest.mark.parametrize("N", [203, 512])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_packed16_step_vs_oracle(gpu, N, mode):
+    """The 16x16 four-boards-a-wave step (k_step_packed, forced below its env-count threshold)
+    directly against the C oracle, not only against k_step: obs, mask, rewards, dones, outcome,
+    labels, counts, mines and RNG state over 120 steps (N = 203 leaves a partial last wave)."""
+    from ms_amd import _lib as L
+    _diff_run(16, 16, 40, N=N, T=120, mode=mode, seed=13, dbg=L.MS_DBG_FORCE_PACKED)
 
 
 def test_packed16_default_dispatch_at_65536(gpu):

@@ -12,6 +12,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 // native vector: HIP's uint4 struct copies through memcpy and is left in scratch
@@ -92,6 +93,20 @@ __device__ __forceinline__ int opaque0() {
 __device__ __forceinline__ float pin_f32(float v) {
   asm("" : "+v"(v));
   return v;
+}
+
+// fmaf(a, (float)h, c) for the low / high fp16 half h of a 32-bit word, as one v_fma_mix_f32:
+// the f16 -> f32 conversion is exact, so it rounds once exactly as the v_cvt_f32_f16 + v_fma_f32
+// pair it replaces (the compiler does not form it from a vector element extraction)
+__device__ __forceinline__ float fmix_lo(float a, uint32_t h2, float c) {
+  float r;
+  asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,0]" : "=v"(r) : "v"(a), "v"(h2), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float fmix_hi(float a, uint32_t h2, float c) {
+  float r;
+  asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(r) : "v"(a), "v"(h2), "v"(c));
+  return r;
 }
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations and

@@ -1486,16 +1486,40 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_bwd(TrunkBwdPar
             }
             const E8 y8 = __builtin_bit_cast(E8, yr[i]);
             const uint32_t pos = mv[u];
+            const u32x4 dw = __builtin_bit_cast(u32x4, d8);
             E8 z8;
+            if constexpr (std::is_same_v<E, _Float16>) {
+              // fp16: every f16 -> f32 widening folded into a v_fma_mix (exact conversion, one
+              // rounding each, so the values are the generic path's bit for bit): d * dmask + (-0)
+              // is the product with its sign of zero, 1 * y - mean the difference, and the sums
+              // take the rounded dz straight from its packed pair (zf + s1, zf * yh + s2)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const float d = (float)d8[j] * dm[j];
-              z8[j] = (E)(((pos >> j) & 1u) ? d : 0.f);
-              const float zf = (float)z8[j];
-              const float yh = ((float)y8[j] - mean) * rstd;
-              s1[j] += zf;
-              s2[j] = __builtin_fmaf(zf, yh, s2[j]);
-              s3[j] += yh;
+              for (int w = 0; w < 4; ++w) {
+                const int j0 = 2 * w, j1 = 2 * w + 1;
+                const float d0 = fmix_lo(dm[j0], dw[w], -0.0f), d1 = fmix_hi(dm[j1], dw[w], -0.0f);
+                const f16x2 zh = {(E)(((pos >> j0) & 1u) ? d0 : 0.f), (E)(((pos >> j1) & 1u) ? d1 : 0.f)};
+                const uint32_t zp = __builtin_bit_cast(uint32_t, zh);
+                const float yh0 = fmix_lo(1.0f, yr[i][w], -mean) * rstd, yh1 = fmix_hi(1.0f, yr[i][w], -mean) * rstd;
+                s1[j0] = fmix_lo(1.0f, zp, s1[j0]);
+                s1[j1] = fmix_hi(1.0f, zp, s1[j1]);
+                s2[j0] = fmix_lo(yh0, zp, s2[j0]);
+                s2[j1] = fmix_hi(yh1, zp, s2[j1]);
+                s3[j0] += yh0;
+                s3[j1] += yh1;
+                z8[j0] = zh[0];
+                z8[j1] = zh[1];
+              }
+            } else {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const float d = (float)d8[j] * dm[j];
+                z8[j] = (E)(((pos >> j) & 1u) ? d : 0.f);
+                const float zf = (float)z8[j];
+                const float yh = ((float)y8[j] - mean) * rstd;
+                s1[j] += zf;
+                s2[j] = __builtin_fmaf(zf, yh, s2[j]);
+                s3[j] += yh;
+              }
             }
             *reinterpret_cast<u32x4*>(sp) = __builtin_bit_cast(u32x4, z8);
           }
@@ -1602,8 +1626,16 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_bwd(TrunkBwdPar
             const E8 z8 = __builtin_bit_cast(E8, zv);
             const E8 y8 = __builtin_bit_cast(E8, yr[i]);
             E8 d8;
+            if constexpr (std::is_same_v<E, _Float16>) {  // the same two fmas, each one v_fma_mix
 #pragma unroll
-            for (int j = 0; j < 8; ++j) d8[j] = (E)__builtin_fmaf(A[j], (float)z8[j], __builtin_fmaf(Bg, (float)y8[j], Cg));
+              for (int w = 0; w < 4; ++w) {
+                d8[2 * w] = (E)fmix_lo(A[2 * w], zv[w], fmix_lo(Bg, yr[i][w], Cg));
+                d8[2 * w + 1] = (E)fmix_hi(A[2 * w + 1], zv[w], fmix_hi(Bg, yr[i][w], Cg));
+              }
+            } else {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) d8[j] = (E)__builtin_fmaf(A[j], (float)z8[j], __builtin_fmaf(Bg, (float)y8[j], Cg));
+            }
             const u32x4 v = __builtin_bit_cast(u32x4, d8);
             *reinterpret_cast<u32x4*>(sp) = v;
 #ifdef MC_DIAG

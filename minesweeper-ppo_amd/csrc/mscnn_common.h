@@ -109,6 +109,19 @@ __device__ __forceinline__ float fmix_hi(float a, uint32_t h2, float c) {
   return r;
 }
 
+// (float)a + (float)b for the low / high fp16 halves of two words, as 1 * a + b in one v_fma_mix_f32
+// (both widenings exact, one rounding: the f32 sum the cvt + cvt + add sequence gives)
+__device__ __forceinline__ float fmix2_lo(uint32_t a2, uint32_t b2) {
+  float r;
+  asm("v_fma_mix_f32 %0, 1.0, %1, %2 op_sel_hi:[0,1,1]" : "=v"(r) : "v"(a2), "v"(b2));
+  return r;
+}
+__device__ __forceinline__ float fmix2_hi(uint32_t a2, uint32_t b2) {
+  float r;
+  asm("v_fma_mix_f32 %0, 1.0, %1, %2 op_sel:[0,1,1] op_sel_hi:[0,1,1]" : "=v"(r) : "v"(a2), "v"(b2));
+  return r;
+}
+
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations and
 // meets the other waves, leaving global loads and stores in flight. __syncthreads()'s
 // workgroup release fence turns into s_waitcnt vmcnt(0) as soon as global stores are

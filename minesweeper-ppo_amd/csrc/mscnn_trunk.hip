@@ -1737,9 +1737,15 @@ __global__ __launch_bounds__(256, NPT <= 2 ? 2 : 1) void k_trunk_bwd(TrunkBwdPar
 #pragma unroll
               for (int e = 0; e < 4; ++e) d4[e] = (E)acc[t][ct][4 * g + e];
               if (addz) {
-                const typename EV<E>::v4 z4 = __builtin_bit_cast(typename EV<E>::v4, zk[HOLD ? t : 0][ct][g]);
+                if constexpr (std::is_same_v<E, _Float16>) {  // 1 * dx + dz, both widened in one v_fma_mix
+                  const u32x2 dp = __builtin_bit_cast(u32x2, d4), zp = zk[HOLD ? t : 0][ct][g];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) d4[e] = (E)pin_f32((float)d4[e] + (float)z4[e]);
+                  for (int e = 0; e < 4; ++e) d4[e] = (E)((e & 1) ? fmix2_hi(dp[e >> 1], zp[e >> 1]) : fmix2_lo(dp[e >> 1], zp[e >> 1]));
+                } else {
+                  const typename EV<E>::v4 z4 = __builtin_bit_cast(typename EV<E>::v4, zk[HOLD ? t : 0][ct][g]);
+#pragma unroll
+                  for (int e = 0; e < 4; ++e) d4[e] = (E)pin_f32((float)d4[e] + (float)z4[e]);
+                }
               }
               *reinterpret_cast<u32x2*>(&sD[px * DCP + ct * 32 + 8 * g + 4 * hh]) = __builtin_bit_cast(u32x2, d4);
             }
